@@ -1,0 +1,165 @@
+/*
+ * pf_engine.h — C ABI of the MI355X SIR particle-filter engine (libpf_hip.so).
+ *
+ * Plain C types only (pointers + sizes); no torch / HIP types cross this line.
+ * Every entry point returns a pf_status (PF_OK == 0); pf_last_error() gives a
+ * thread-local message for the last failure.  Host arrays are caller-owned and
+ * copied in/out; device buffers are owned by the handle.  One handle = one
+ * device + one HIP stream, not re-entrant; separate handles may be driven from
+ * separate threads.
+ *
+ * Each entry replaces a piece of the reference's Python filter
+ * (/root/reference/models/particle_filter.py, cited "pf.py:LINE"); the Python
+ * mirror particle_filters_amd/particle_filter.py binds them via ctypes (see
+ * INTEGRATION.md for the binding a maintainer of the reference would add).
+ */
+#ifndef PF_ENGINE_H
+#define PF_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t pf_status;
+#define PF_OK 0
+#define PF_E_NOT_INITIALIZED 1 /* -> AssertionError("Filter not initialized.") pf.py:142,231,252 */
+#define PF_E_ARG 2             /* bad shape / argument -> ValueError */
+#define PF_E_NOT_PD 3          /* Cholesky failed -> numpy.linalg.LinAlgError */
+#define PF_E_HIP 4             /* HIP runtime error */
+#define PF_E_UNSUPPORTED 5     /* model shape not compiled into this library */
+
+/* g: transition kinds (pf.py:237 per-particle g(x,u)) */
+#define PF_TRANS_LINEAR 0 /* x' = A x (+ u)                         params: A[nx*nx]         */
+#define PF_TRANS_L96 1    /* one RK4 step of Lorenz-96              params: F, dt            */
+/* h: observation kinds (pf.py:257 per-particle h(x)) */
+#define PF_OBS_LINEAR 0   /* z = H x + c                            params: H[nz*nx], c[nz]  */
+#define PF_OBS_EXP_HALF 1 /* z_k = beta_k exp(x_k / 2)   (nz==nx)   params: beta[nz]         */
+#define PF_OBS_ACOUSTIC 2 /* z_s = sum_c psi/(|p_c-s|^2+d0) (nx=4C) params: psi, d0, sx[nz], sy[nz] */
+
+#define PF_RESAMPLE_SYSTEMATIC 0 /* pf.py:146-171 */
+#define PF_RESAMPLE_MULTINOMIAL 1 /* pf.py:173-186 (any other method string) */
+
+#define PF_PRECISION_FP32 0
+#define PF_PRECISION_FP64 1
+
+typedef struct pf_model_desc {
+  int32_t nx, nz;
+  int32_t trans_kind, obs_kind;
+  const double* trans_params; /* see PF_TRANS_* */
+  int64_t n_trans_params;
+  const double* obs_params;   /* see PF_OBS_* */
+  int64_t n_obs_params;
+  const double* Q; /* nx*nx process-noise covariance (pf.py:94) */
+  const double* R; /* nz*nz measurement-noise covariance (pf.py:95) */
+} pf_model_desc;
+
+typedef struct pf_opts {
+  int64_t n_particles;     /* Np (pf.py:96) */
+  int32_t n_replicates;    /* independent filters batched in one launch (>= 1) */
+  int32_t resample_method; /* PF_RESAMPLE_* (pf.py:98, 205-208) */
+  double resample_thresh;  /* resample when Neff < thresh * Np (pf.py:97, 204) */
+  int32_t regularize;      /* jitter 0.001*chol(Q) n after resampling (pf.py:99, 212-218) */
+  int32_t precision;       /* PF_PRECISION_* : particle storage / arithmetic type */
+  uint64_t seed;           /* Philox key; replicate r uses counter word r */
+  int32_t device;          /* HIP device ordinal */
+  int32_t replicate_base;  /* global id of local replicate 0: replicate r draws with counter
+                              word replicate_base + r, so sharding replicates over GPUs gives
+                              bitwise the same per-replicate results as one GPU */
+} pf_opts;
+
+typedef struct pf_handle pf_handle;
+
+/* Per-replicate posterior summary of one update (pf.py:262-268). */
+typedef struct pf_update_info {
+  double neff;     /* pre-resample 1/sum w^2 (pf.py:203) */
+  double log_norm; /* log sum_i w_{t-1,i} exp(-quad_i/2): marginal-likelihood increment */
+  int32_t resample; /* 1 if Neff < thresh*Np (the resample is applied by pf_resample) */
+  int32_t _pad;
+} pf_update_info;
+
+const char* pf_last_error(void);
+const char* pf_version(void);
+int32_t pf_device_count(void);
+
+/* ParticleFilter.__init__ (pf.py:79-107): validates the model, factorises R
+ * (+1e-12 I) and Q (+1e-10 I / +1e-12 I fallbacks), allocates device state. */
+pf_status pf_create(const pf_model_desc* model, const pf_opts* opts, pf_handle** out);
+void pf_destroy(pf_handle* h);
+/* Is (nx, nz, trans_kind, obs_kind) compiled into this library? */
+int32_t pf_model_supported(int32_t nx, int32_t nz, int32_t trans_kind, int32_t obs_kind);
+
+/* initialize (pf.py:110-132): particles ~ N(mean_r, cov_r), uniform weights.
+ * mean [R][nx], cov [R][nx][nx]; replay_normals [R][N][nx] or NULL (device Philox). */
+pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, const double* replay_normals);
+
+/* predict (pf.py:223-237): x <- g(x, u) + chol(Q) n.  u [R][nx] or NULL;
+ * replay_normals [R][N][nx] or NULL. */
+pf_status pf_predict(pf_handle* h, const double* u, const double* replay_normals);
+
+/* update, weighting half (pf.py:253-264 up to the resample decision).
+ * z [R][nz]; info [R] out (nullable); mean [R][nx], cov [R][nx][nx] out (nullable):
+ * the weighted posterior (the reported state when no resample happens). */
+pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double* mean, double* cov);
+
+/* _resample, applying half (pf.py:204-218): replicates whose last update decided to
+ * resample get their ancestors gathered (+ jitter); weights become uniform.
+ * uniforms: NULL (device Philox) or [R] systematic U / [R][N] multinomial u;
+ * jitter_normals [R][N][nx] or NULL.  mean/cov out (nullable): uniform-weight
+ * statistics of the resampled set (pf.py:266-267), written for resampled replicates. */
+pf_status pf_resample(pf_handle* h, const double* uniforms, const double* jitter_normals, double* mean,
+                      double* cov);
+
+/* Force a resample of the current (set_state) particles with their weights, whatever
+ * Neff is: the applying half of ParticleFilter._resample(particles, weights) once the
+ * caller has made the Neff test itself (pf.py:203-218).  uniforms / jitter as in
+ * pf_resample (NULL = device Philox). */
+pf_status pf_resample_state(pf_handle* h, const double* uniforms, const double* jitter_normals);
+
+/* The device-resident T loop: for t in [0,T): step(Z[t], U[t]) — or update(Z[0]) first
+ * when first_update_only (notebook driver, PF_VS_experiments.ipynb cell 7) — with no
+ * host synchronisation inside T.  Z [T][R][nz]; U [T][R][nx] or NULL.
+ * Outputs (host, nullable): means [T][R][nx] (post-resample when resampled, as the
+ * reference's PFState.mean), covs [T][R][nx][nx] (nx <= 4), neff [T][R] (pre-resample),
+ * flags [T][R], log_norm [T][R]. */
+pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int32_t first_update_only,
+                 double* means, double* covs, double* neff, uint8_t* flags, double* log_norm);
+
+/* Same, with every array already in device memory (HBM-resident inputs and outputs;
+ * Z/U in the engine precision).  No host copies, no synchronisation: returns after
+ * enqueueing on the handle's stream.  flags are int32 [T][R]. */
+pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t first_update_only,
+                        double* d_means, double* d_covs, double* d_neff, int32_t* d_flags,
+                        double* d_log_norm);
+
+/* State readout / injection.  particles [R][N][nx] (AoS like PFState.particles);
+ * log_weights [R][N] normalised (log w); weights [R][N]. */
+pf_status pf_get_particles(pf_handle* h, double* particles);
+pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights);
+pf_status pf_set_state(pf_handle* h, const double* particles, const double* weights);
+int32_t pf_weights_uniform(pf_handle* h);
+
+/* Weighted mean/cov of the current state, exact two-pass (np.average / np.cov
+ * aweights, bias=True; pf.py:266-267), any nx.  mean [R][nx], cov [R][nx][nx]. */
+pf_status pf_moments(pf_handle* h, double* mean, double* cov);
+
+/* Standalone resampling of caller weights (pf.py:146-186 _systematic_resample /
+ * _multinomial_resample).  w [N] normalised; method PF_RESAMPLE_*; systematic uses U,
+ * multinomial uses uniforms [N].  idx [N] int64 out. */
+pf_status pf_resample_indices(int32_t device, int32_t method, const double* w, int64_t N, double U,
+                              const double* uniforms, int64_t* idx);
+
+/* Measurement hooks for bench.py: the handle's HIP stream (hipStream_t as void*),
+ * synchronisation, and per-launch device durations of `steps` step-kernels timed
+ * with HIP events on that stream (ms_out [steps]). */
+void* pf_stream(pf_handle* h);
+pf_status pf_synchronize(pf_handle* h);
+pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* ms_out);
+/* Geometry of the step launch: tiles per replicate, tile size, dynamic LDS bytes. */
+pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PF_ENGINE_H */

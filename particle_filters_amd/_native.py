@@ -1,0 +1,139 @@
+"""ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C
+particle_filters_amd/csrc``).  There is no fallback: if the library is missing
+or cannot be loaded, importing the engine raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpf_hip.so")
+
+PF_OK = 0
+PF_E_NOT_INITIALIZED = 1
+PF_E_ARG = 2
+PF_E_NOT_PD = 3
+PF_E_HIP = 4
+PF_E_UNSUPPORTED = 5
+
+PF_TRANS_LINEAR = 0
+PF_TRANS_L96 = 1
+PF_OBS_LINEAR = 0
+PF_OBS_EXP_HALF = 1
+PF_OBS_ACOUSTIC = 2
+PF_RESAMPLE_SYSTEMATIC = 0
+PF_RESAMPLE_MULTINOMIAL = 1
+PF_PRECISION_FP32 = 0
+PF_PRECISION_FP64 = 1
+
+_dp = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("nz", C.c_int32), ("trans_kind", C.c_int32), ("obs_kind", C.c_int32),
+                ("trans_params", _dp), ("n_trans_params", C.c_int64),
+                ("obs_params", _dp), ("n_obs_params", C.c_int64),
+                ("Q", _dp), ("R", _dp)]
+
+
+class Opts(C.Structure):
+    _fields_ = [("n_particles", C.c_int64), ("n_replicates", C.c_int32), ("resample_method", C.c_int32),
+                ("resample_thresh", C.c_double), ("regularize", C.c_int32), ("precision", C.c_int32),
+                ("seed", C.c_uint64), ("device", C.c_int32), ("replicate_base", C.c_int32)]
+
+
+class UpdateInfo(C.Structure):
+    _fields_ = [("neff", C.c_double), ("log_norm", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/pf_engine.h
+SIGNATURES = {
+    "pf_last_error": (C.c_char_p, []),
+    "pf_version": (C.c_char_p, []),
+    "pf_device_count": (C.c_int32, []),
+    "pf_model_supported": (C.c_int32, [C.c_int32] * 4),
+    "pf_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(Opts), C.POINTER(_vp)]),
+    "pf_destroy": (None, [_vp]),
+    "pf_initialize": (C.c_int32, [_vp, _dp, _dp, _dp]),
+    "pf_predict": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_update": (C.c_int32, [_vp, _dp, C.POINTER(UpdateInfo), _dp, _dp]),
+    "pf_resample": (C.c_int32, [_vp, _dp, _dp, _dp, _dp]),
+    "pf_resample_state": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_run": (C.c_int32, [_vp, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp, C.POINTER(C.c_uint8), _dp]),
+    "pf_run_device": (C.c_int32, [_vp, _vp, _vp, C.c_int64, C.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "pf_get_particles": (C.c_int32, [_vp, _dp]),
+    "pf_get_weights": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_set_state": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_weights_uniform": (C.c_int32, [_vp]),
+    "pf_moments": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_resample_indices": (C.c_int32, [C.c_int32, C.c_int32, _dp, C.c_int64, C.c_double, _dp,
+                                        C.POINTER(C.c_int64)]),
+    "pf_stream": (_vp, [_vp]),
+    "pf_synchronize": (C.c_int32, [_vp]),
+    "pf_profile_steps": (C.c_int32, [_vp, _vp, C.c_int64, C.POINTER(C.c_float)]),
+    "pf_geometry": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> C.CDLL:
+    """Load libpf_hip.so (raises ImportError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: build the HIP engine first "
+                "(python -c 'import __graft_entry__ as g; g.build()' or make -C particle_filters_amd/csrc)")
+        lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+class PFError(RuntimeError):
+    pass
+
+
+def check(status: int, what: str = "") -> None:
+    """Map a pf_status to the reference's exception types (particle_filter.py)."""
+    if status == PF_OK:
+        return
+    msg = load().pf_last_error().decode(errors="replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if status == PF_E_NOT_INITIALIZED:
+        raise AssertionError("Filter not initialized.")
+    if status == PF_E_NOT_PD:
+        raise np.linalg.LinAlgError(msg)
+    if status == PF_E_ARG:
+        raise ValueError(msg)
+    if status == PF_E_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise PFError(msg)
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 array (or NULL for None)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def device_count() -> int:
+    return int(load().pf_device_count())

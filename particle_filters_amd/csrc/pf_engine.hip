@@ -1,0 +1,963 @@
+// Host side of the MI355X SIR engine: the C ABI of include/pf_engine.h.
+//
+// Owns one device, one HIP stream and the device-resident filter state of R
+// replicates; turns the reference's call sequence (initialize / predict /
+// update / _resample, /root/reference/models/particle_filter.py:110-287) into
+// launches of the fused kernels in pf_kernels.h, and runs the whole T loop on
+// device (pf_run_device) with no host synchronisation inside T.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pf_engine.h"
+#include "pf_ops.h"
+#include "pf_resample_w.h"
+
+namespace pf {
+
+static thread_local std::string g_err;
+
+static pf_status fail(pf_status code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(PF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+static std::vector<Ops>& registry() {
+  static std::vector<Ops> r;
+  return r;
+}
+void register_ops(const Ops& o) { registry().push_back(o); }
+static void ensure_registered() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    register_sv_models();
+    register_linear_models();
+    register_l96_models();
+    register_mat_models();
+  });
+}
+const Ops* find_ops(int nx, int nz, int tk, int ok, int prec) {
+  ensure_registered();
+  for (const Ops& o : registry())
+    if (o.nx == nx && o.nz == nz && o.tk == tk && o.ok == ok && o.prec == prec) return &o;
+  return nullptr;
+}
+
+// Lower Cholesky factor of an n x n row-major SPD matrix (+ jitter * I); false if not PD.
+static bool cholesky(const double* A, int n, double jitter, std::vector<double>& L) {
+  L.assign((size_t)n * n, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = A[j * n + j] + jitter;
+    for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+    if (!(d > 0.0) || !std::isfinite(d)) return false;
+    const double ljj = std::sqrt(d);
+    L[j * n + j] = ljj;
+    for (int i = j + 1; i < n; ++i) {
+      double s = A[i * n + j] + (i == j ? jitter : 0.0);
+      for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = s / ljj;
+    }
+  }
+  return true;
+}
+
+}  // namespace pf
+
+using namespace pf;
+
+struct pf_handle {
+  const Ops* ops = nullptr;
+  int nx = 0, nz = 0, tk = 0, ok = 0, prec = 0;
+  int64_t N = 0, Npad = 0;
+  int R = 1, G = 1, tile = 0, method = 0, regularize = 0, r_diag = 1;
+  double thresh = 0.5;
+  uint64_t seed = 0;
+  int device = 0;
+  int rep_base = 0;
+  size_t esz = 4;  // sizeof(Real)
+  hipStream_t stream = nullptr;
+  // device state
+  void* x[2] = {nullptr, nullptr};
+  void* lw[2] = {nullptr, nullptr};
+  double* rec[2] = {nullptr, nullptr};
+  int cx = 0, clw = 0, crec = 0;
+  void* P = nullptr;   // model params (Real)
+  double* cdf = nullptr;
+  // small device staging
+  void* d_z = nullptr;       // Real [R][nz]
+  void* d_u = nullptr;       // Real [R][nx]
+  double* d_out = nullptr;   // API outputs: mean[R*nx] cov[R*nx*nx] neff[R] lse[R] flags(int)[R] + post
+  double* d_replay_a = nullptr;  // [R][N][nx] normals
+  double* d_replay_b = nullptr;  // [R][N][nx] jitter normals
+  double* d_unif = nullptr;      // [R][N] uniforms
+  // host-side bookkeeping
+  bool initialized = false;
+  bool pending = false;       // last update decided to resample some replicate (not yet applied)
+  uint32_t epoch = 1;         // Philox epoch counter (one per predict, one per update)
+  uint32_t ep_res = 0;        // epoch reserved by the last update for its resample
+  bool chol_q_ok = true;
+  std::vector<double> Pd;     // params (double)
+};
+
+namespace {
+
+size_t rec_bytes(const pf_handle* h) { return (size_t)h->R * h->G * h->ops->rec_size * sizeof(double); }
+
+void choose_geometry(pf_handle* h) {
+  const int ch = h->ops->ch;
+  const int tile_min = BLOCK * ch;
+  const int tile_max = h->ops->tile_max;
+  const char* env = std::getenv("PF_BLOCKS_TARGET");
+  const int64_t target_blocks = env ? std::max(1, std::atoi(env)) : 256;
+  int64_t G = std::max<int64_t>(1, (target_blocks + h->R - 1) / h->R);
+  G = std::min<int64_t>(G, (h->N + tile_min - 1) / tile_min);
+  G = std::max<int64_t>(G, (h->N + tile_max - 1) / tile_max);
+  G = std::max<int64_t>(1, std::min<int64_t>(G, MAXG));
+  int64_t tile = (h->N + G - 1) / G;
+  tile = (tile + ch - 1) / ch * ch;
+  if (tile > tile_max) tile = tile_max;
+  h->tile = (int)tile;
+  h->G = (int)((h->N + tile - 1) / tile);
+}
+
+size_t step_lds(const pf_handle* h, bool sys_gather) {
+  const size_t area = std::max<size_t>(sys_gather ? (size_t)h->tile : 0, (size_t)NWAVES * h->ops->rec_size);
+  return base_lds_bytes() + area * sizeof(double);
+}
+
+template <typename T>
+void to_real(const double* src, size_t n, std::vector<char>& dst, size_t esz) {
+  dst.resize(n * esz);
+  if (esz == 8) {
+    std::memcpy(dst.data(), src, n * 8);
+  } else {
+    float* f = (float*)dst.data();
+    for (size_t i = 0; i < n; ++i) f[i] = (float)src[i];
+  }
+}
+
+StepParams base_params(pf_handle* h) {
+  StepParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.P = h->P;
+  p.N = h->N;
+  p.Npad = h->Npad;
+  p.G = h->G;
+  p.tile = h->tile;
+  p.seed = h->seed;
+  p.thresh = h->thresh;
+  p.method = h->method;
+  p.regularize = h->regularize;
+  p.r_diag = h->r_diag;
+  p.rep_base = h->rep_base;
+  p.out_step = -1;
+  p.out_post_step = -1;
+  p.z_rs = h->nz;
+  p.u_rs = h->nx;
+  return p;
+}
+
+// API output slots inside d_out
+struct OutSlots {
+  double *mean, *cov, *neff, *lse;
+  int32_t* flag;
+};
+OutSlots out_slots(pf_handle* h) {
+  OutSlots s;
+  s.mean = h->d_out;
+  s.cov = s.mean + (size_t)h->R * h->nx;
+  s.neff = s.cov + (size_t)h->R * h->nx * h->nx;
+  s.lse = s.neff + h->R;
+  s.flag = (int32_t*)(s.lse + h->R);
+  return s;
+}
+size_t out_doubles(const pf_handle* h) {
+  return (size_t)h->R * h->nx + (size_t)h->R * h->nx * h->nx + 2 * (size_t)h->R + (size_t)h->R;
+}
+
+void set_outputs(StepParams& p, const OutSlots& s, bool cov_ok) {
+  p.o_mean = s.mean;
+  p.o_cov = cov_ok ? s.cov : nullptr;
+  p.o_neff = s.neff;
+  p.o_lse = s.lse;
+  p.o_flag = s.flag;
+}
+
+pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw, bool writes_rec) {
+  p.x_in = h->x[h->cx];
+  p.x_out = h->x[h->cx ^ 1];
+  p.lw_in = h->lw[h->clw];
+  p.lw_out = h->lw[h->clw ^ 1];
+  p.rec_in = h->rec[h->crec];
+  p.rec_out = h->rec[h->crec ^ 1];
+  const bool sys_gather = p.allow_gather && h->method == 0;
+  dim3 grid((unsigned)h->G, (unsigned)h->R);
+  HIPCHK(h->ops->step(p, grid, step_lds(h, sys_gather), h->stream));
+  if (writes_x) h->cx ^= 1;
+  if (writes_lw) h->clw ^= 1;
+  if (writes_rec) h->crec ^= 1;
+  return PF_OK;
+}
+
+pf_status launch_cdf(pf_handle* h, StepParams p) {
+  p.rec_in = h->rec[h->crec];
+  p.lw_in = h->lw[h->clw];
+  dim3 grid((unsigned)h->G, (unsigned)h->R);
+  HIPCHK(h->ops->cdf(p, h->cdf, grid, base_lds_bytes() + (size_t)h->tile * sizeof(double), h->stream));
+  return PF_OK;
+}
+
+pf_status launch_finalize(pf_handle* h, StepParams p) {
+  p.rec_in = h->rec[h->crec];
+  HIPCHK(h->ops->finalize(p, h->R, h->stream));
+  return PF_OK;
+}
+
+pf_status upload_real(pf_handle* h, void* dst, const double* src, size_t n) {
+  std::vector<char> buf;
+  to_real<double>(src, n, buf, h->esz);
+  HIPCHK(hipMemcpyAsync(dst, buf.data(), n * h->esz, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));  // buf is pageable & local
+  return PF_OK;
+}
+
+pf_status ensure_replay(pf_handle* h, double** buf, size_t n) {
+  if (!*buf) HIPCHK(hipMalloc((void**)buf, n * sizeof(double)));
+  return PF_OK;
+}
+
+// Apply a resample decided by the last update (gather-only launch) + finalize aux stats.
+pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitter, bool want_stats,
+                        bool force = false) {
+  StepParams p = base_params(h);
+  p.force_gather = force;
+  const size_t nrep = (size_t)h->R * h->N;
+  if (uniforms) {
+    const size_t n = h->method == 0 ? (size_t)h->R : nrep;
+    pf_status st = ensure_replay(h, &h->d_unif, nrep > (size_t)h->R ? nrep : (size_t)h->R);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(h->d_unif, uniforms, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    p.rp_unif = h->d_unif;
+  }
+  if (jitter && h->regularize) {
+    pf_status st = ensure_replay(h, &h->d_replay_b, nrep * h->nx);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(h->d_replay_b, jitter, nrep * h->nx * sizeof(double), hipMemcpyHostToDevice,
+                          h->stream));
+    p.rp_jit = h->d_replay_b;
+  }
+  p.cdf = h->cdf;
+  p.allow_gather = 1;
+  p.ep_resample = h->ep_res;
+  if (h->method == 1) {
+    pf_status st = launch_cdf(h, p);
+    if (st) return st;
+  }
+  pf_status st = launch_step(h, p, true, false, true);
+  if (st) return st;
+  h->pending = false;
+  if (want_stats) {
+    StepParams f = base_params(h);
+    set_outputs(f, out_slots(h), h->nx <= 4);
+    f.out_post_step = 0;
+    st = launch_finalize(h, f);
+    if (st) return st;
+  }
+  if (uniforms || jitter) HIPCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pf_last_error(void) { return g_err.c_str(); }
+const char* pf_version(void) { return "particle_filters_amd 0.1 (gfx950)"; }
+
+int32_t pf_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int32_t pf_model_supported(int32_t nx, int32_t nz, int32_t tk, int32_t ok) {
+  return find_ops(nx, nz, tk, ok, PF_PRECISION_FP32) != nullptr;
+}
+
+pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
+  if (!m || !o || !out) return fail(PF_E_ARG, "null argument");
+  *out = nullptr;
+  if (m->nx <= 0 || m->nz <= 0) return fail(PF_E_ARG, "nx and nz must be positive");
+  if (o->n_particles <= 0) return fail(PF_E_ARG, "n_particles must be positive");
+  if (o->n_replicates <= 0) return fail(PF_E_ARG, "n_replicates must be positive");
+  if (o->precision != PF_PRECISION_FP32 && o->precision != PF_PRECISION_FP64)
+    return fail(PF_E_ARG, "precision must be PF_PRECISION_FP32 or PF_PRECISION_FP64");
+  const Ops* ops = find_ops(m->nx, m->nz, m->trans_kind, m->obs_kind, o->precision);
+  if (!ops)
+    return fail(PF_E_UNSUPPORTED, "model (nx=" + std::to_string(m->nx) + ", nz=" + std::to_string(m->nz) +
+                                      ", g=" + std::to_string(m->trans_kind) + ", h=" +
+                                      std::to_string(m->obs_kind) + ") is not compiled into libpf_hip");
+  const int nx = m->nx, nz = m->nz;
+  // ---- parameters (double, host) -------------------------------------------
+  std::vector<double> P((size_t)ops->psize, 0.0);
+  auto lay_A = 0, lay_LQ = nx * nx, lay_LJ = 2 * nx * nx, lay_H = 3 * nx * nx, lay_C = lay_H + nz * nx,
+       lay_LR = lay_C + nz, lay_EX = lay_LR + nz * nz;
+  if (m->trans_kind == PF_TRANS_LINEAR) {
+    if (m->n_trans_params < (int64_t)nx * nx || !m->trans_params) return fail(PF_E_ARG, "LINEAR g needs A[nx*nx]");
+    for (int i = 0; i < nx * nx; ++i) P[lay_A + i] = m->trans_params[i];
+  } else if (m->trans_kind == PF_TRANS_L96) {
+    if (m->n_trans_params < 2 || !m->trans_params) return fail(PF_E_ARG, "L96 g needs {F, dt}");
+    P[lay_EX + 0] = m->trans_params[0];
+    P[lay_EX + 1] = m->trans_params[1];
+  }
+  if (m->obs_kind == PF_OBS_LINEAR) {
+    if (m->n_obs_params < (int64_t)nz * nx + nz || !m->obs_params) return fail(PF_E_ARG, "LINEAR h needs H[nz*nx], c[nz]");
+    for (int i = 0; i < nz * nx; ++i) P[lay_H + i] = m->obs_params[i];
+    for (int i = 0; i < nz; ++i) P[lay_C + i] = m->obs_params[nz * nx + i];
+  } else if (m->obs_kind == PF_OBS_EXP_HALF) {
+    if (m->n_obs_params < nz || !m->obs_params) return fail(PF_E_ARG, "EXP_HALF h needs beta[nz]");
+    for (int i = 0; i < nz; ++i) P[lay_C + i] = m->obs_params[i];
+  } else if (m->obs_kind == PF_OBS_ACOUSTIC) {
+    if (m->n_obs_params < 2 + 2 * nz || !m->obs_params) return fail(PF_E_ARG, "ACOUSTIC h needs psi, d0, sx[nz], sy[nz]");
+    for (int i = 0; i < 2 + 2 * nz; ++i) P[lay_EX + i] = m->obs_params[i];
+  }
+  if (!m->Q || !m->R) return fail(PF_E_ARG, "Q and R are required");
+  std::vector<double> L;
+  // LR = chol(R + 1e-12 I)  (particle_filter.py:107)
+  if (!cholesky(m->R, nz, 1e-12, L)) return fail(PF_E_NOT_PD, "Matrix is not positive definite (R)");
+  int r_diag = 1;
+  for (int i = 0; i < nz; ++i)
+    for (int j = 0; j < nz; ++j) {
+      P[lay_LR + i * nz + j] = L[i * nz + j];
+      if (i != j && L[i * nz + j] != 0.0) r_diag = 0;
+    }
+  // predict: chol(Q), fallback chol(Q + 1e-10 I)  (particle_filter.py:232-235)
+  bool qok = cholesky(m->Q, nx, 0.0, L) || cholesky(m->Q, nx, 1e-10, L);
+  if (qok)
+    for (int i = 0; i < nx * nx; ++i) P[lay_LQ + i] = L[i];
+  // jitter: 0.001 * (chol(Q), fallback chol(Q + 1e-12 I))  (particle_filter.py:213-217)
+  if (cholesky(m->Q, nx, 0.0, L) || cholesky(m->Q, nx, 1e-12, L))
+    for (int i = 0; i < nx * nx; ++i) P[lay_LJ + i] = 0.001 * L[i];
+
+  HIPCHK(hipSetDevice(o->device));
+  pf_handle* h = new pf_handle();
+  h->ops = ops;
+  h->nx = nx; h->nz = nz; h->tk = m->trans_kind; h->ok = m->obs_kind; h->prec = o->precision;
+  h->N = o->n_particles;
+  h->Npad = (o->n_particles + 3) / 4 * 4;
+  h->R = o->n_replicates;
+  h->method = o->resample_method == PF_RESAMPLE_SYSTEMATIC ? 0 : 1;
+  h->thresh = o->resample_thresh;
+  h->regularize = o->regularize != 0;
+  h->seed = o->seed;
+  h->device = o->device;
+  h->rep_base = o->replicate_base;
+  h->esz = o->precision == PF_PRECISION_FP64 ? 8 : 4;
+  h->r_diag = r_diag;
+  h->chol_q_ok = qok;
+  h->Pd = P;
+  choose_geometry(h);
+  ops->prepare();
+  auto cleanup = [&](pf_status st) {
+    pf_destroy(h);
+    return st;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(PF_E_HIP, "hipStreamCreate failed"));
+  const size_t xbytes = (size_t)h->R * nx * h->Npad * h->esz;
+  const size_t lwbytes = (size_t)h->R * h->Npad * h->esz;
+  for (int k = 0; k < 2; ++k) {
+    if (hipMalloc(&h->x[k], xbytes) != hipSuccess || hipMalloc(&h->lw[k], lwbytes) != hipSuccess ||
+        hipMalloc((void**)&h->rec[k], rec_bytes(h)) != hipSuccess)
+      return cleanup(fail(PF_E_HIP, "hipMalloc of particle state failed"));
+    (void)hipMemset(h->x[k], 0, xbytes);
+    (void)hipMemset(h->lw[k], 0, lwbytes);
+  }
+  if (h->method == 1 && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
+    return cleanup(fail(PF_E_HIP, "hipMalloc of cdf failed"));
+  if (hipMalloc(&h->P, P.size() * h->esz) != hipSuccess || hipMalloc(&h->d_z, (size_t)h->R * nz * h->esz) != hipSuccess ||
+      hipMalloc(&h->d_u, (size_t)h->R * nx * h->esz) != hipSuccess ||
+      hipMalloc((void**)&h->d_out, out_doubles(h) * sizeof(double)) != hipSuccess)
+    return cleanup(fail(PF_E_HIP, "hipMalloc of parameters failed"));
+  if (upload_real(h, h->P, P.data(), P.size()) != PF_OK) return cleanup(PF_E_HIP);
+  *out = h;
+  return PF_OK;
+}
+
+void pf_destroy(pf_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (int k = 0; k < 2; ++k) {
+    if (h->x[k]) (void)hipFree(h->x[k]);
+    if (h->lw[k]) (void)hipFree(h->lw[k]);
+    if (h->rec[k]) (void)hipFree(h->rec[k]);
+  }
+  for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
+                  (void*)h->d_replay_b, (void*)h->d_unif})
+    if (p) (void)hipFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, const double* replay) {
+  if (!h || !mean || !cov) return fail(PF_E_ARG, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  const int nx = h->nx, R = h->R;
+  // Lc = chol(cov + 1e-10 I)  (particle_filter.py:127)
+  std::vector<double> Lc((size_t)R * nx * nx), L;
+  for (int r = 0; r < R; ++r) {
+    if (!cholesky(cov + (size_t)r * nx * nx, nx, 1e-10, L))
+      return fail(PF_E_NOT_PD, "Matrix is not positive definite (initial covariance)");
+    std::copy(L.begin(), L.end(), Lc.begin() + (size_t)r * nx * nx);
+  }
+  void *dmean = nullptr, *dL = nullptr;
+  HIPCHK(hipMalloc(&dmean, (size_t)R * nx * h->esz));
+  HIPCHK(hipMalloc(&dL, (size_t)R * nx * nx * h->esz));
+  pf_status st = upload_real(h, dmean, mean, (size_t)R * nx);
+  if (!st) st = upload_real(h, dL, Lc.data(), Lc.size());
+  const double* drep = nullptr;
+  if (!st && replay) {
+    st = ensure_replay(h, &h->d_replay_a, (size_t)R * h->N * nx);
+    if (!st && hipMemcpy(h->d_replay_a, replay, (size_t)R * h->N * nx * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      st = fail(PF_E_HIP, "replay upload failed");
+    drep = h->d_replay_a;
+  }
+  if (!st) {
+    const uint32_t ep = h->epoch++;
+    hipError_t e = h->ops->init(h->x[h->cx ^ 1], h->rec[h->crec ^ 1], dmean, dL, drep, h->N, h->Npad, h->G, R,
+                                h->seed, ep, h->rep_base, h->stream);
+    if (e != hipSuccess) st = fail(PF_E_HIP, std::string("init launch: ") + hipGetErrorString(e));
+    h->cx ^= 1;
+    h->crec ^= 1;
+  }
+  (void)hipStreamSynchronize(h->stream);
+  (void)hipFree(dmean);
+  (void)hipFree(dL);
+  if (st) return st;
+  h->initialized = true;
+  h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  if (!h->chol_q_ok) return fail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
+  HIPCHK(hipSetDevice(h->device));
+  StepParams p = base_params(h);
+  if (u) {
+    pf_status st = upload_real(h, h->d_u, u, (size_t)h->R * h->nx);
+    if (st) return st;
+    p.u = h->d_u;
+  }
+  if (replay) {
+    pf_status st = ensure_replay(h, &h->d_replay_a, (size_t)h->R * h->N * h->nx);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(h->d_replay_a, replay, (size_t)h->R * h->N * h->nx * sizeof(double),
+                          hipMemcpyHostToDevice, h->stream));
+    p.rp_noise = h->d_replay_a;
+  }
+  // a resample decided but not yet applied is fused into this launch
+  const bool gather = h->pending;
+  if (gather && h->method == 1) {
+    pf_status st = launch_cdf(h, p);
+    if (st) return st;
+  }
+  p.allow_gather = gather;
+  p.ep_resample = h->ep_res;
+  p.cdf = h->cdf;
+  p.do_predict = 1;
+  p.ep_predict = h->epoch++;
+  pf_status st = launch_step(h, p, true, false, gather);
+  h->pending = false;
+  if (replay || u) HIPCHK(hipStreamSynchronize(h->stream));
+  return st;
+}
+
+pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double* mean, double* cov) {
+  if (!h || !z) return fail(PF_E_ARG, "null argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->pending) {  // an earlier decision nobody applied: apply it before re-weighting
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  pf_status st = upload_real(h, h->d_z, z, (size_t)h->R * h->nz);
+  if (st) return st;
+  StepParams p = base_params(h);
+  p.z = h->d_z;
+  p.do_update = 1;
+  st = launch_step(h, p, false, true, true);
+  if (st) return st;
+  h->ep_res = h->epoch++;
+  StepParams f = base_params(h);
+  set_outputs(f, out_slots(h), h->nx <= 4);
+  f.out_step = 0;
+  f.allow_gather = 1;
+  st = launch_finalize(h, f);
+  if (st) return st;
+  std::vector<double> buf(out_doubles(h));
+  HIPCHK(hipMemcpyAsync(buf.data(), h->d_out, buf.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int R = h->R, nx = h->nx;
+  const double* bm = buf.data();
+  const double* bc = bm + (size_t)R * nx;
+  const double* bn = bc + (size_t)R * nx * nx;
+  const double* bl = bn + R;
+  const int32_t* bf = (const int32_t*)(bl + R);
+  bool any = false;
+  for (int r = 0; r < R; ++r) {
+    if (info) {
+      info[r].neff = bn[r];
+      info[r].log_norm = bl[r];
+      info[r].resample = bf[r];
+      info[r]._pad = 0;
+    }
+    any = any || bf[r];
+  }
+  if (mean) std::memcpy(mean, bm, (size_t)R * nx * sizeof(double));
+  if (cov) {
+    if (nx <= 4) {
+      std::memcpy(cov, bc, (size_t)R * nx * nx * sizeof(double));
+    } else {
+      st = pf_moments(h, nullptr, cov);
+      if (st) return st;
+    }
+  }
+  h->pending = any;
+  return PF_OK;
+}
+
+pf_status pf_resample(pf_handle* h, const double* uniforms, const double* jitter, double* mean, double* cov) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  if (!h->pending) return PF_OK;
+  HIPCHK(hipSetDevice(h->device));
+  pf_status st = apply_pending(h, uniforms, jitter, true);
+  if (st) return st;
+  if (mean || cov) {
+    std::vector<double> buf(out_doubles(h));
+    HIPCHK(hipMemcpyAsync(buf.data(), h->d_out, buf.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const size_t nm = (size_t)h->R * h->nx;
+    if (mean) std::memcpy(mean, buf.data(), nm * sizeof(double));
+    if (cov) {
+      if (h->nx <= 4) {
+        std::memcpy(cov, buf.data() + nm, nm * h->nx * sizeof(double));
+      } else {
+        st = pf_moments(h, nullptr, cov);
+        if (st) return st;
+      }
+    }
+  }
+  return PF_OK;
+}
+
+pf_status pf_resample_state(pf_handle* h, const double* uniforms, const double* jitter) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  h->ep_res = h->epoch++;
+  pf_status st = apply_pending(h, uniforms, jitter, false, true);
+  if (st) return st;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t first_update_only,
+                        double* d_means, double* d_covs, double* d_neff, int32_t* d_flags, double* d_lse) {
+  if (!h || !dZ || T <= 0) return fail(PF_E_ARG, "bad argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  if (!d_means || !d_neff || !d_flags || !d_lse) return fail(PF_E_ARG, "device outputs are required");
+  if (!h->chol_q_ok) return fail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
+  HIPCHK(hipSetDevice(h->device));
+  const int R = h->R;
+  StepParams p = base_params(h);
+  p.o_mean = d_means;
+  p.o_cov = (h->nx <= 4) ? d_covs : nullptr;
+  p.o_neff = d_neff;
+  p.o_lse = d_lse;
+  p.o_flag = d_flags;
+  p.cdf = h->cdf;
+  p.do_update = 1;
+  bool gather_possible = h->pending;  // a pre-run decision is applied by kernel 0
+  uint32_t prev_res = h->ep_res;
+  for (int64_t s = 0; s < T; ++s) {
+    const bool predict = !(first_update_only && s == 0);
+    p.z = (const char*)dZ + (size_t)s * R * h->nz * h->esz;
+    p.u = dU ? (const char*)dU + (size_t)s * R * h->nx * h->esz : nullptr;
+    p.do_predict = predict;
+    p.ep_predict = predict ? h->epoch++ : 0;
+    p.allow_gather = gather_possible;
+    p.ep_resample = prev_res;
+    p.out_step = s >= 1 ? s - 1 : -1;
+    p.out_post_step = s >= 2 ? s - 2 : -1;
+    if (gather_possible && h->method == 1) {
+      pf_status st = launch_cdf(h, p);
+      if (st) return st;
+    }
+    pf_status st = launch_step(h, p, predict || gather_possible, true, true);
+    if (st) return st;
+    prev_res = h->epoch++;
+    gather_possible = true;
+  }
+  h->ep_res = prev_res;
+  // tail: outputs of the last update, its resample (if any) and that resample's stats
+  p.z = nullptr;
+  p.u = nullptr;
+  p.do_predict = 0;
+  p.do_update = 0;
+  p.allow_gather = 1;
+  p.ep_resample = prev_res;
+  p.out_step = T - 1;
+  p.out_post_step = T >= 2 ? T - 2 : -1;
+  if (h->method == 1) {
+    pf_status st = launch_cdf(h, p);
+    if (st) return st;
+  }
+  pf_status st = launch_step(h, p, true, false, true);
+  if (st) return st;
+  p.out_step = -1;
+  p.out_post_step = T - 1;
+  st = launch_finalize(h, p);
+  if (st) return st;
+  h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int32_t first_update_only,
+                 double* means, double* covs, double* neff, uint8_t* flags, double* lse) {
+  if (!h || !Z || T <= 0) return fail(PF_E_ARG, "bad argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  const int R = h->R, nx = h->nx, nz = h->nz;
+  void *dZ = nullptr, *dU = nullptr;
+  double *dm = nullptr, *dc = nullptr, *dn = nullptr, *dl = nullptr;
+  int32_t* df = nullptr;
+  pf_status st = PF_OK;
+  auto bail = [&](pf_status s) {
+    (void)hipStreamSynchronize(h->stream);
+    for (void* q : {dZ, dU, (void*)dm, (void*)dc, (void*)dn, (void*)dl, (void*)df})
+      if (q) (void)hipFree(q);
+    return s;
+  };
+  if (hipMalloc(&dZ, (size_t)T * R * nz * h->esz) != hipSuccess ||
+      (U && hipMalloc(&dU, (size_t)T * R * nx * h->esz) != hipSuccess) ||
+      hipMalloc((void**)&dm, (size_t)T * R * nx * sizeof(double)) != hipSuccess ||
+      (covs && nx <= 4 && hipMalloc((void**)&dc, (size_t)T * R * nx * nx * sizeof(double)) != hipSuccess) ||
+      hipMalloc((void**)&dn, (size_t)T * R * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&dl, (size_t)T * R * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&df, (size_t)T * R * sizeof(int32_t)) != hipSuccess)
+    return bail(fail(PF_E_HIP, "hipMalloc for pf_run buffers failed"));
+  st = upload_real(h, dZ, Z, (size_t)T * R * nz);
+  if (!st && U) st = upload_real(h, dU, U, (size_t)T * R * nx);
+  if (st) return bail(st);
+  st = pf_run_device(h, dZ, dU, T, first_update_only, dm, dc, dn, df, dl);
+  if (st) return bail(st);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(PF_E_HIP, "pf_run: stream sync failed"));
+  std::vector<int32_t> fl((size_t)T * R);
+  if ((means && hipMemcpy(means, dm, (size_t)T * R * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (covs && dc && hipMemcpy(covs, dc, (size_t)T * R * nx * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (neff && hipMemcpy(neff, dn, (size_t)T * R * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (lse && hipMemcpy(lse, dl, (size_t)T * R * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      hipMemcpy(fl.data(), df, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return bail(fail(PF_E_HIP, "pf_run: output copy failed"));
+  if (flags)
+    for (size_t i = 0; i < fl.size(); ++i) flags[i] = (uint8_t)(fl[i] != 0);
+  return bail(PF_OK);
+}
+
+static pf_status download_real(pf_handle* h, const void* src, size_t n, std::vector<double>& out) {
+  out.resize(n);
+  if (h->esz == 8) {
+    HIPCHK(hipMemcpyAsync(out.data(), src, n * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  } else {
+    std::vector<float> f(n);
+    HIPCHK(hipMemcpyAsync(f.data(), src, n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (size_t i = 0; i < n; ++i) out[i] = (double)f[i];
+  }
+  return PF_OK;
+}
+
+pf_status pf_get_particles(pf_handle* h, double* particles) {
+  if (!h || !particles) return fail(PF_E_ARG, "null argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->pending) {
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  std::vector<double> soa;
+  pf_status st = download_real(h, h->x[h->cx], (size_t)h->R * h->nx * h->Npad, soa);
+  if (st) return st;
+  const int nx = h->nx;
+  for (int r = 0; r < h->R; ++r)
+    for (int d = 0; d < nx; ++d) {
+      const double* src = soa.data() + ((size_t)r * nx + d) * h->Npad;
+      double* dst = particles + (size_t)r * h->N * nx + d;
+      for (int64_t i = 0; i < h->N; ++i) dst[i * nx] = src[i];
+    }
+  return PF_OK;
+}
+
+int32_t pf_weights_uniform(pf_handle* h) {
+  if (!h || !h->initialized) return 0;
+  if (h->pending) {
+    if (apply_pending(h, nullptr, nullptr, false) != PF_OK) return 0;
+  }
+  int32_t all = 1;
+  for (int r = 0; r < h->R; ++r) {
+    double u = 0.0;
+    if (hipMemcpy(&u, h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3, sizeof(double),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return 0;
+    all = all && (u != 0.0);
+  }
+  return all;
+}
+
+pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
+  if (!h) return fail(PF_E_ARG, "null argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->pending) {
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  // per-replicate normaliser from the current records (k_finalize into scratch)
+  StepParams f = base_params(h);
+  set_outputs(f, out_slots(h), false);
+  f.out_step = 0;
+  pf_status st = launch_finalize(h, f);
+  if (st) return st;
+  std::vector<double> buf(out_doubles(h));
+  HIPCHK(hipMemcpyAsync(buf.data(), h->d_out, buf.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  std::vector<double> uni(h->R);
+  for (int r = 0; r < h->R; ++r)
+    HIPCHK(hipMemcpyAsync(&uni[r], h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3, sizeof(double),
+                          hipMemcpyDeviceToHost, h->stream));
+  std::vector<double> lw;
+  st = download_real(h, h->lw[h->clw], (size_t)h->R * h->Npad, lw);
+  if (st) return st;
+  const double* lse = buf.data() + (size_t)h->R * h->nx + (size_t)h->R * h->nx * h->nx + h->R;
+  for (int r = 0; r < h->R; ++r) {
+    for (int64_t i = 0; i < h->N; ++i) {
+      const size_t o = (size_t)r * h->N + i;
+      double l;
+      if (uni[r] != 0.0) {
+        if (weights) weights[o] = 1.0 / (double)h->N;
+        l = -std::log((double)h->N);
+      } else {
+        l = lw[(size_t)r * h->Npad + i] - lse[r];
+        if (weights) weights[o] = std::exp(l);
+      }
+      if (log_weights) log_weights[o] = l;
+    }
+  }
+  return PF_OK;
+}
+
+pf_status pf_set_state(pf_handle* h, const double* particles, const double* weights) {
+  if (!h || !particles) return fail(PF_E_ARG, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  const int nx = h->nx, R = h->R;
+  std::vector<double> soa((size_t)R * nx * h->Npad, 0.0);
+  for (int r = 0; r < R; ++r)
+    for (int d = 0; d < nx; ++d)
+      for (int64_t i = 0; i < h->N; ++i)
+        soa[((size_t)r * nx + d) * h->Npad + i] = particles[((size_t)r * h->N + i) * nx + d];
+  pf_status st = upload_real(h, h->x[h->cx], soa.data(), soa.size());
+  if (st) return st;
+  // records: one tile carrying S0 = 1 at m = 0 (so lse = 0), the rest empty; or uniform
+  std::vector<double> rec((size_t)R * h->G * h->ops->rec_size, 0.0);
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < h->G; ++k) {
+      double* o = rec.data() + ((size_t)r * h->G + k) * h->ops->rec_size;
+      if (!weights) {
+        o[3] = 1.0;
+      } else {
+        o[0] = k == 0 ? 0.0 : -INFINITY;
+        o[1] = k == 0 ? 1.0 : 0.0;
+        o[2] = k == 0 ? 1.0 : 0.0;
+      }
+    }
+  HIPCHK(hipMemcpy(h->rec[h->crec], rec.data(), rec.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (weights) {
+    std::vector<double> lw((size_t)R * h->Npad, -INFINITY);
+    for (int r = 0; r < R; ++r)
+      for (int64_t i = 0; i < h->N; ++i) lw[(size_t)r * h->Npad + i] = std::log(weights[(size_t)r * h->N + i]);
+    st = upload_real(h, h->lw[h->clw], lw.data(), lw.size());
+    if (st) return st;
+    // re-derive proper per-tile records: an update launch with no likelihood term
+    StepParams p = base_params(h);
+    p.do_update = 2;  // 2 = reweigh only (log-likelihood skipped)
+    p.z = h->d_z;
+    st = launch_step(h, p, false, true, true);
+    if (st) return st;
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->initialized = true;
+  h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_moments(pf_handle* h, double* mean, double* cov) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->pending) {
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  // lse of the current records -> scratch, then two-pass moments on device
+  StepParams f = base_params(h);
+  OutSlots o = out_slots(h);
+  set_outputs(f, o, false);
+  f.out_step = 0;
+  pf_status st = launch_finalize(h, f);
+  if (st) return st;
+  const int nx = h->nx, R = h->R;
+  double *dmean = nullptr, *dcov = nullptr;
+  HIPCHK(hipMalloc((void**)&dmean, (size_t)R * nx * sizeof(double)));
+  if (cov && hipMalloc((void**)&dcov, (size_t)R * nx * nx * sizeof(double)) != hipSuccess) {
+    (void)hipFree(dmean);
+    return fail(PF_E_HIP, "hipMalloc failed");
+  }
+  hipError_t e = h->ops->moments(h->x[h->cx], h->lw[h->clw], h->rec[h->crec], h->G, o.lse, h->N, h->Npad, R, dmean,
+                                 dcov, h->stream);
+  if (e == hipSuccess && mean)
+    e = hipMemcpyAsync(mean, dmean, (size_t)R * nx * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && cov)
+    e = hipMemcpyAsync(cov, dcov, (size_t)R * nx * nx * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(dmean);
+  if (dcov) (void)hipFree(dcov);
+  if (e != hipSuccess) return fail(PF_E_HIP, std::string("pf_moments: ") + hipGetErrorString(e));
+  return PF_OK;
+}
+
+pf_status pf_resample_indices(int32_t device, int32_t method, const double* w, int64_t N, double U,
+                              const double* uniforms, int64_t* idx) {
+  if (!w || !idx || N <= 0) return fail(PF_E_ARG, "bad argument");
+  if (method == 1 && !uniforms) return fail(PF_E_ARG, "multinomial needs uniforms");
+  HIPCHK(hipSetDevice(device));
+  const int tile = 4096;
+  const int G = (int)((N + tile - 1) / tile);
+  if (G > 4 * BLOCK) return fail(PF_E_ARG, "N too large for pf_resample_indices");
+  double *dw = nullptr, *dsum = nullptr, *dcdf = nullptr, *du = nullptr;
+  int64_t* didx = nullptr;
+  auto done = [&](pf_status s) {
+    for (void* q : {(void*)dw, (void*)dsum, (void*)dcdf, (void*)du, (void*)didx})
+      if (q) (void)hipFree(q);
+    return s;
+  };
+  if (hipMalloc((void**)&dw, N * 8) != hipSuccess || hipMalloc((void**)&dsum, G * 8) != hipSuccess ||
+      hipMalloc((void**)&dcdf, N * 8) != hipSuccess || hipMalloc((void**)&didx, N * 8) != hipSuccess ||
+      (method == 1 && hipMalloc((void**)&du, N * 8) != hipSuccess))
+    return done(fail(PF_E_HIP, "hipMalloc failed"));
+  if (hipMemcpy(dw, w, N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      (du && hipMemcpy(du, uniforms, N * 8, hipMemcpyHostToDevice) != hipSuccess))
+    return done(fail(PF_E_HIP, "upload failed"));
+  hipLaunchKernelGGL(k_w_tile_sums, dim3(G), dim3(BLOCK), 64 * 8, 0, dw, N, tile, dsum);
+  hipLaunchKernelGGL(k_w_cdf, dim3(G), dim3(BLOCK), 64 * 8, 0, dw, N, tile, G, dsum, dcdf, method == 0);
+  hipLaunchKernelGGL(k_w_search, dim3((unsigned)((N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0, dcdf, N, method, U,
+                     du, didx);
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return done(fail(PF_E_HIP, "resample kernels failed"));
+  if (hipMemcpy(idx, didx, N * 8, hipMemcpyDeviceToHost) != hipSuccess) return done(fail(PF_E_HIP, "download failed"));
+  return done(PF_OK);
+}
+
+void* pf_stream(pf_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+pf_status pf_synchronize(pf_handle* h) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (G) *G = h->G;
+  if (tile) *tile = h->tile;
+  if (lds) *lds = (int32_t)step_lds(h, h->method == 0);
+  return PF_OK;
+}
+
+pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* ms_out) {
+  if (!h || !dZ || steps <= 0 || !ms_out) return fail(PF_E_ARG, "bad argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  const int R = h->R;
+  double *dm = nullptr, *dn = nullptr, *dl = nullptr;
+  int32_t* df = nullptr;
+  HIPCHK(hipMalloc((void**)&dm, (size_t)steps * R * h->nx * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&dn, (size_t)steps * R * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&dl, (size_t)steps * R * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&df, (size_t)steps * R * sizeof(int32_t)));
+  std::vector<hipEvent_t> ev((size_t)steps + 1);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  StepParams p = base_params(h);
+  p.o_mean = dm;
+  p.o_neff = dn;
+  p.o_lse = dl;
+  p.o_flag = df;
+  p.cdf = h->cdf;
+  p.do_update = 1;
+  p.do_predict = 1;
+  bool gather_possible = h->pending;
+  uint32_t prev_res = h->ep_res;
+  pf_status st = PF_OK;
+  for (int64_t s = 0; s < steps && !st; ++s) {
+    p.z = (const char*)dZ + (size_t)s * R * h->nz * h->esz;
+    p.ep_predict = h->epoch++;
+    p.allow_gather = gather_possible;
+    p.ep_resample = prev_res;
+    p.out_step = s >= 1 ? s - 1 : -1;
+    p.out_post_step = s >= 2 ? s - 2 : -1;
+    if (gather_possible && h->method == 1) st = launch_cdf(h, p);
+    if (!st) {
+      (void)hipEventRecord(ev[s], h->stream);
+      st = launch_step(h, p, true, true, true);
+    }
+    prev_res = h->epoch++;
+    gather_possible = true;
+  }
+  (void)hipEventRecord(ev[steps], h->stream);
+  (void)hipStreamSynchronize(h->stream);
+  h->ep_res = prev_res;
+  h->pending = false;
+  // leave a consistent state: apply the last decision
+  if (!st) {
+    StepParams q = base_params(h);
+    q.allow_gather = 1;
+    q.ep_resample = prev_res;
+    q.cdf = h->cdf;
+    if (h->method == 1) st = launch_cdf(h, q);
+    if (!st) st = launch_step(h, q, true, false, true);
+  }
+  (void)hipStreamSynchronize(h->stream);
+  for (int64_t s = 0; s < steps; ++s) (void)hipEventElapsedTime(&ms_out[s], ev[s], ev[s + 1]);
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  for (void* q : {(void*)dm, (void*)dn, (void*)dl, (void*)df}) (void)hipFree(q);
+  return st;
+}
+
+}  // extern "C"

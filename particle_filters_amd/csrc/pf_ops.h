@@ -1,0 +1,101 @@
+// Type-erased launchers for one compiled model shape (nx, nz, g kind, h kind,
+// precision).  Each pf_inst_*.hip translation unit instantiates the kernel
+// templates for its model family and registers an Ops entry; pf_engine.hip
+// looks the entry up at pf_create time.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "pf_kernels.h"
+
+namespace pf {
+
+struct Ops {
+  int nx, nz, tk, ok, prec;
+  int rec_size, ch, tile_max, psize;
+  hipError_t (*step)(const StepParams&, dim3, size_t, hipStream_t);
+  hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
+  hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
+  hipError_t (*init)(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
+                     int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, hipStream_t);
+  hipError_t (*moments)(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,
+                        int64_t Npad, int R, double* mean, double* cov, hipStream_t);
+  void (*prepare)();  // per-device kernel attributes, called once a device is current
+};
+
+void register_ops(const Ops& o);
+const Ops* find_ops(int nx, int nz, int tk, int ok, int prec);
+
+inline size_t base_lds_bytes() { return (size_t)(64 + MAXG + 8) * sizeof(double); }
+
+template <typename Real, int NX, int NZ, int TK, int OK>
+struct Launch {
+  static hipError_t step(const StepParams& p, dim3 grid, size_t smem, hipStream_t s) {
+    hipLaunchKernelGGL((k_step<Real, NX, NZ, TK, OK>), grid, dim3(BLOCK), smem, s, p);
+    return hipGetLastError();
+  }
+  static hipError_t finalize(const StepParams& p, int R, hipStream_t s) {
+    hipLaunchKernelGGL((k_finalize<NX>), dim3(R), dim3(BLOCK), 64 * sizeof(double), s, p);
+    return hipGetLastError();
+  }
+  static hipError_t cdf(const StepParams& p, double* out, dim3 grid, size_t smem, hipStream_t s) {
+    hipLaunchKernelGGL((k_cdf<Real, NX>), grid, dim3(BLOCK), smem, s, p, out);
+    return hipGetLastError();
+  }
+  static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
+                         int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch,
+                         int rep_base, hipStream_t s) {
+    const int64_t n = N > G ? N : G;
+    dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK), (unsigned)R);
+    hipLaunchKernelGGL((k_init<Real, NX>), grid, dim3(BLOCK), 0, s, (Real*)x, rec, (const Real*)mean,
+                       (const Real*)Lc, replay, N, Npad, G, seed, epoch, rep_base);
+    return hipGetLastError();
+  }
+  static hipError_t moments(const void* x, const void* lw, const double* rec, int G, const double* lse,
+                            int64_t N, int64_t Npad, int R, double* mean, double* cov, hipStream_t s) {
+    hipLaunchKernelGGL((k_mom_mean<Real, NX>), dim3(NX, R), dim3(BLOCK), 64 * sizeof(double), s, (const Real*)x,
+                       (const Real*)lw, rec, Rec<NX>::SIZE, G, lse, N, Npad, mean);
+    if (cov)
+      hipLaunchKernelGGL((k_mom_cov<Real, NX>), dim3(NX * NX, R), dim3(BLOCK), 64 * sizeof(double), s,
+                         (const Real*)x, (const Real*)lw, rec, Rec<NX>::SIZE, G, lse, N, Npad, mean, cov);
+    return hipGetLastError();
+  }
+  static Ops make(int prec) {
+    Ops o;
+    o.nx = NX; o.nz = NZ; o.tk = TK; o.ok = OK; o.prec = prec;
+    o.rec_size = Rec<NX>::SIZE;
+    o.ch = StepTraits<Real, NX, NZ, TK, OK>::CH;
+    o.tile_max = StepTraits<Real, NX, NZ, TK, OK>::TILE_MAX;
+    o.psize = ParamLayout<NX, NZ>::SIZE;
+    o.step = &step;
+    o.finalize = &finalize;
+    o.cdf = &cdf;
+    o.init = &init;
+    o.moments = &moments;
+    o.prepare = &prepare;
+    return o;
+  }
+  static void prepare() {
+    // allow up to 160 KiB of dynamic LDS for the tile CDF
+    (void)hipFuncSetAttribute((const void*)k_step<Real, NX, NZ, TK, OK>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_cdf<Real, NX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+  }
+};
+
+// explicit registration (called once from pf_engine.hip; no static-init order games)
+void register_sv_models();
+void register_linear_models();
+void register_l96_models();
+void register_mat_models();
+
+template <int NX, int NZ, int TK, int OK>
+inline void register_both() {
+  register_ops(Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32));
+  register_ops(Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64));
+}
+
+}  // namespace pf

@@ -1,0 +1,117 @@
+// Counter-based Philox4x32-10 (Salmon et al., SC'11) and Box-Muller normals.
+//
+// Every random number of the SIR step is a pure function of
+//   key     = (seed_lo, seed_hi)
+//   counter = (group index, replicate, epoch, stream)
+// so any lane can draw its own numbers with no state and no ordering between
+// workgroups: the same (seed, replicate) reproduces bit-identically whatever the
+// grid, the replicate-to-GPU sharding or the call pattern (predict/update split
+// vs the fused device-resident T loop).
+//
+// "group index" enumerates the normals of a draw in NumPy's row-major order
+// (particle i, state dim d) -> flat f = i*nx + d: one Philox call yields the
+// 4 normals f = 4g..4g+3 (two Box-Muller pairs).  fp32 and fp64 engines use the
+// same 32-bit uniforms; only the Box-Muller arithmetic precision differs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pf {
+
+enum : uint32_t {
+  STREAM_INIT = 1,      // initialize(): particles ~ N(mean, cov)
+  STREAM_PROCESS = 2,   // predict(): process noise
+  STREAM_JITTER = 3,    // post-resample regularisation
+  STREAM_RESAMPLE = 4,  // systematic U / multinomial uniforms
+};
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// Uniform in (0, 1] from 32 random bits (never 0, so log() is finite).
+__device__ __forceinline__ float u01_f32(uint32_t a) {
+  return ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ double u01_f64(uint32_t a) {
+  return ((double)a + 1.0) * (1.0 / 4294967296.0);
+}
+// Uniform in [0, 1) with 53 bits from two words (systematic U, multinomial u).
+__host__ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return (double)(((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+template <typename Real>
+struct Normal4 {
+  Real v[4];
+};
+
+// Box-Muller on the two pairs (x, y) and (z, w): r = sqrt(-2 ln u1), angle 2*pi*u2.
+__device__ __forceinline__ Normal4<float> box_muller4(u32x4 r) {
+  Normal4<float> n;
+  const float r0 = sqrtf(-2.0f * __logf(u01_f32(r.x)));
+  const float r1 = sqrtf(-2.0f * __logf(u01_f32(r.z)));
+  float s0, c0, s1, c1;
+  sincospif((float)(r.y >> 8) * (2.0f / 16777216.0f), &s0, &c0);
+  sincospif((float)(r.w >> 8) * (2.0f / 16777216.0f), &s1, &c1);
+  n.v[0] = r0 * c0;
+  n.v[1] = r0 * s0;
+  n.v[2] = r1 * c1;
+  n.v[3] = r1 * s1;
+  return n;
+}
+__device__ __forceinline__ Normal4<double> box_muller4_f64(u32x4 r) {
+  Normal4<double> n;
+  const double r0 = sqrt(-2.0 * log(u01_f64(r.x)));
+  const double r1 = sqrt(-2.0 * log(u01_f64(r.z)));
+  double s0, c0, s1, c1;
+  sincospi((double)(r.y >> 8) * (2.0 / 16777216.0), &s0, &c0);
+  sincospi((double)(r.w >> 8) * (2.0 / 16777216.0), &s1, &c1);
+  n.v[0] = r0 * c0;
+  n.v[1] = r0 * s0;
+  n.v[2] = r1 * c1;
+  n.v[3] = r1 * s1;
+  return n;
+}
+
+template <typename Real>
+__device__ __forceinline__ Normal4<Real> normal4(uint64_t seed, uint32_t group, uint32_t rep,
+                                                 uint32_t epoch, uint32_t stream);
+template <>
+__device__ __forceinline__ Normal4<float> normal4<float>(uint64_t seed, uint32_t group, uint32_t rep,
+                                                         uint32_t epoch, uint32_t stream) {
+  return box_muller4(philox4x32_10(u32x4{group, rep, epoch, stream}, (uint32_t)seed,
+                                   (uint32_t)(seed >> 32)));
+}
+template <>
+__device__ __forceinline__ Normal4<double> normal4<double>(uint64_t seed, uint32_t group, uint32_t rep,
+                                                           uint32_t epoch, uint32_t stream) {
+  return box_muller4_f64(philox4x32_10(u32x4{group, rep, epoch, stream}, (uint32_t)seed,
+                                       (uint32_t)(seed >> 32)));
+}
+
+// One [0,1) double per (index, replicate, epoch) on the resample stream.
+__host__ __device__ __forceinline__ double uniform53(uint64_t seed, uint32_t index, uint32_t rep,
+                                                     uint32_t epoch) {
+  u32x4 r = philox4x32_10(u32x4{index, rep, epoch, STREAM_RESAMPLE}, (uint32_t)seed,
+                          (uint32_t)(seed >> 32));
+  return u53(r.x, r.y);
+}
+
+}  // namespace pf

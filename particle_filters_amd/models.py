@@ -1,0 +1,267 @@
+"""Device state-space-model plugins: the ``g`` / ``h`` arguments of ``ParticleFilter``.
+
+The reference passes arbitrary Python callables ``g(x, u) -> (nx,)`` and
+``h(x) -> (nz,)`` (``/root/reference/models/particle_filter.py:20-22``) and calls
+them once per particle (``:237``, ``:257``).  A GPU cannot call Python per
+particle, so the engine takes *model objects* that
+
+* describe the function to the HIP kernels (a kind + parameters, see
+  ``include/pf_engine.h`` ``PF_TRANS_*`` / ``PF_OBS_*``), and
+* are still callables with the reference's per-particle semantics, so the very
+  same objects can be handed to the reference's own ``ParticleFilter``.
+
+The wirings the reference uses map to one-liners:
+
+======================================================  =========================================
+reference closure                                        here
+======================================================  =========================================
+``lambda x, u: alpha * x`` (SV, test_pf_vs_simulator_sv.py:50)     ``SVTransition(alpha)``
+``lambda x: beta*np.exp(0.5*x)`` (:54)                    ``ExpHalfObservation(beta)``
+log-squared ``log b^2 + x + E`` (PF_VS notebook cell 6)   ``SVLogSqObservation(beta)``
+``A @ x (+u)`` / ``H @ x`` (test_pf_shapes_and_api.py)   ``LinearTransition(A)`` / ``LinearObservation(H)``
+``rk4_step(x, dt, l96_rhs)`` / ``x[H_idx]`` (L96)         ``L96Transition(F, dt, nx)`` / ``SelectObservation(H_idx, nx)``
+MAT joint ``g_joint`` / ``h_joint``                      ``CVTransition(C, dt)`` / ``AcousticObservation(S, psi, d0, C)``
+======================================================  =========================================
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+
+# E[log chi^2_1] = digamma(1/2) - log(1/2), Var = polygamma(1, 1/2) = pi^2/2
+LOGCHI2_MEAN = -1.2703628454614782
+LOGCHI2_VAR = 4.934802200544679
+
+
+class Transition:
+    kind: int
+    nx: int
+
+    def params(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def __call__(self, x, u=None):  # per particle, reference semantics
+        raise NotImplementedError
+
+
+class Observation:
+    kind: int
+    nx: int
+    nz: int
+
+    def params(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def __call__(self, x):
+        raise NotImplementedError
+
+
+# ---------------------------------------------------------------------------
+# transitions
+# ---------------------------------------------------------------------------
+class LinearTransition(Transition):
+    """``g(x, u) = A x (+ u)``."""
+
+    kind = N.PF_TRANS_LINEAR
+
+    def __init__(self, A):
+        self.A = np.atleast_2d(np.asarray(A, float))
+        if self.A.shape[0] != self.A.shape[1]:
+            raise ValueError("A must be square")
+        self.nx = self.A.shape[0]
+
+    def params(self):
+        return np.ascontiguousarray(self.A.ravel())
+
+    def __call__(self, x, u=None):
+        x = np.asarray(x, float)
+        return self.A @ x if u is None else self.A @ x + u
+
+
+class SVTransition(LinearTransition):
+    """Stochastic-volatility AR(1): ``g(x) = alpha * x`` (elementwise for vector alpha)."""
+
+    def __init__(self, alpha):
+        self.alpha = np.atleast_1d(np.asarray(alpha, float))
+        super().__init__(np.diag(self.alpha))
+
+    def __call__(self, x, u=None):
+        x = np.atleast_1d(np.asarray(x, float))
+        y = self.alpha * x
+        return y if u is None else y + u
+
+
+class CVTransition(LinearTransition):
+    """Joint constant-velocity dynamics of ``n_targets`` ``[x, y, vx, vy]`` blocks
+    (simulator_Multi_acoustic_tracking.py:77-101; MAT notebook ``g_joint``)."""
+
+    def __init__(self, n_targets: int = 4, dt: float = 1.0):
+        F = np.eye(4)
+        F[0, 2] = dt
+        F[1, 3] = dt
+        self.n_targets = n_targets
+        self.F = F
+        super().__init__(np.kron(np.eye(n_targets), F))
+
+    def __call__(self, x, u=None):
+        x = np.asarray(x, float)
+        out = np.zeros(4 * self.n_targets)
+        for c in range(self.n_targets):
+            out[4 * c:4 * c + 4] = self.F @ x[4 * c:4 * c + 4]
+        return out if u is None else out + u
+
+
+class L96Transition(Transition):
+    """One RK4 step of Lorenz-96 (simulator_Lorenz_96.py:35-84)."""
+
+    kind = N.PF_TRANS_L96
+
+    def __init__(self, F: float = 8.0, dt: float = 0.01, nx: int = 40):
+        self.F = float(F)
+        self.dt = float(dt)
+        self.nx = int(nx)
+
+    def params(self):
+        return np.array([self.F, self.dt])
+
+    def _rhs(self, x):
+        return (np.roll(x, -1) - np.roll(x, 2)) * np.roll(x, 1) - x + self.F
+
+    def __call__(self, x, u=None):
+        x = np.asarray(x, float)
+        dt = self.dt
+        k1 = self._rhs(x)
+        k2 = self._rhs(x + 0.5 * dt * k1)
+        k3 = self._rhs(x + 0.5 * dt * k2)
+        k4 = self._rhs(x + dt * k3)
+        y = x + (dt / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
+        return y if u is None else y + u
+
+
+# ---------------------------------------------------------------------------
+# observations
+# ---------------------------------------------------------------------------
+class LinearObservation(Observation):
+    """``h(x) = H x + c``."""
+
+    kind = N.PF_OBS_LINEAR
+
+    def __init__(self, H, c=None):
+        self.H = np.atleast_2d(np.asarray(H, float))
+        self.nz, self.nx = self.H.shape
+        self.c = np.zeros(self.nz) if c is None else np.atleast_1d(np.asarray(c, float))
+
+    def params(self):
+        return np.ascontiguousarray(np.r_[self.H.ravel(), self.c])
+
+    def __call__(self, x):
+        return self.H @ np.asarray(x, float) + self.c
+
+
+class SVLogSqObservation(LinearObservation):
+    """Log-squared SV wiring ``h(x) = log(beta^2) + x + E[log chi^2_1]`` — observations
+    must be ``log(Y**2)``, ``R = pi^2/2`` (PF_VS_experiments.ipynb cell 6)."""
+
+    def __init__(self, beta: float):
+        self.beta = float(beta)
+        self.log_beta_sq = float(np.log(self.beta ** 2))
+        super().__init__(np.eye(1), [self.log_beta_sq + LOGCHI2_MEAN])
+
+    def __call__(self, x):
+        x = np.atleast_1d(np.asarray(x, float))
+        return self.log_beta_sq + x + LOGCHI2_MEAN
+
+
+class SelectObservation(LinearObservation):
+    """Partial observation ``h(x) = x[H_idx]`` (simulator_Lorenz_96.py:147-161)."""
+
+    def __init__(self, H_idx, nx: int):
+        self.H_idx = np.asarray(H_idx, dtype=int)
+        H = np.zeros((self.H_idx.size, nx))
+        H[np.arange(self.H_idx.size), self.H_idx] = 1.0
+        super().__init__(H)
+
+    def __call__(self, x):
+        return np.asarray(x, float)[self.H_idx]
+
+
+class ExpHalfObservation(Observation):
+    """``h(x) = beta * exp(x / 2)`` elementwise (SV standard / test-harness wiring)."""
+
+    kind = N.PF_OBS_EXP_HALF
+
+    def __init__(self, beta):
+        self.beta = np.atleast_1d(np.asarray(beta, float))
+        self.nx = self.nz = self.beta.size
+
+    def params(self):
+        return np.ascontiguousarray(self.beta)
+
+    def __call__(self, x):
+        x = np.atleast_1d(np.asarray(x, float))
+        return self.beta * np.exp(0.5 * x)
+
+
+class AcousticObservation(Observation):
+    """Summed acoustic amplitudes ``z_s = sum_c psi / (|p_c - s|^2 + d0)`` of
+    ``n_targets`` ``[x, y, vx, vy]`` blocks (simulator_Multi_acoustic_tracking.py:273-309;
+    MAT notebook ``h_joint``)."""
+
+    kind = N.PF_OBS_ACOUSTIC
+
+    def __init__(self, sensors, psi: float = 10.0, d0: float = 0.1, n_targets: int = 4):
+        self.S = np.asarray(sensors, float).reshape(-1, 2)
+        self.psi = float(psi)
+        self.d0 = float(d0)
+        self.n_targets = int(n_targets)
+        self.nz = self.S.shape[0]
+        self.nx = 4 * self.n_targets
+
+    def params(self):
+        return np.ascontiguousarray(np.r_[self.psi, self.d0, self.S[:, 0], self.S[:, 1]])
+
+    def __call__(self, x):
+        x = np.asarray(x, float)
+        z = np.zeros(self.nz)
+        for c in range(self.n_targets):
+            pos = x[4 * c:4 * c + 2]
+            zc = np.zeros(self.nz)
+            for s in range(self.nz):
+                zc[s] = self.psi / (np.sum((pos - self.S[s]) ** 2) + self.d0)
+            z += zc
+        return z
+
+
+def is_device_model(g, h) -> bool:
+    return isinstance(g, Transition) and isinstance(h, Observation)
+
+
+def describe(g: Transition, h: Observation, Q: np.ndarray, R: np.ndarray):
+    """Validate the pair against Q/R and return (ModelDesc, keepalive arrays)."""
+    nx = Q.shape[0]
+    nz = R.shape[0]
+    if g.nx != nx:
+        raise ValueError(f"g has state dimension {g.nx}, Q is {Q.shape}")
+    if h.nx != nx:
+        raise ValueError(f"h expects state dimension {h.nx}, Q is {Q.shape}")
+    if h.nz != nz:
+        raise ValueError(f"h has observation dimension {h.nz}, R is {R.shape}")
+    tp = np.ascontiguousarray(g.params(), dtype=float)
+    op = np.ascontiguousarray(h.params(), dtype=float)
+    Qc = np.ascontiguousarray(Q, dtype=float)
+    Rc = np.ascontiguousarray(R, dtype=float)
+    d = N.ModelDesc(nx, nz, g.kind, h.kind, N.dptr(tp), tp.size, N.dptr(op), op.size, N.dptr(Qc), N.dptr(Rc))
+    return d, (tp, op, Qc, Rc)
+
+
+def supported(g: Transition, h: Observation) -> bool:
+    return bool(N.load().pf_model_supported(g.nx, h.nz, g.kind, h.kind))
+
+
+def sv_logsq_observations(Y) -> np.ndarray:
+    """``Z = log(Y^2)`` for :class:`SVLogSqObservation`."""
+    return np.log(np.asarray(Y, float) ** 2)
