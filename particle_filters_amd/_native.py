@@ -14,7 +14,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpf_hip.so")
+LIB_PATH = os.environ.get("PF_LIB", os.path.join(_HERE, "libpf_hip.so"))
 
 PF_OK = 0
 PF_E_NOT_INITIALIZED = 1

@@ -117,26 +117,27 @@ namespace {
 
 size_t rec_bytes(const pf_handle* h) { return (size_t)h->R * h->G * h->ops->rec_size * sizeof(double); }
 
-void choose_geometry(pf_handle* h) {
-  const int ch = h->ops->ch;
-  const int tile_min = BLOCK * ch;
-  const int tile_max = h->ops->tile_max;
-  const char* env = std::getenv("PF_BLOCKS_TARGET");
-  const int64_t target_blocks = env ? std::max(1, std::atoi(env)) : 256;
-  int64_t G = std::max<int64_t>(1, (target_blocks + h->R - 1) / h->R);
-  G = std::min<int64_t>(G, (h->N + tile_min - 1) / tile_min);
-  G = std::max<int64_t>(G, (h->N + tile_max - 1) / tile_max);
-  G = std::max<int64_t>(1, std::min<int64_t>(G, MAXG));
-  int64_t tile = (h->N + G - 1) / G;
-  tile = (tile + ch - 1) / ch * ch;
-  if (tile > tile_max) tile = tile_max;
+// Tiles of one chunk per thread (BLOCK*CH particles) so that a large filter runs
+// several workgroups per CU; past MAXG tiles the tile grows (chunks per thread).
+// PF_CHUNKS_PER_THREAD overrides the chunks per thread (tuning experiments).
+bool choose_geometry(pf_handle* h) {
+  const int64_t tile_min = h->ops->tile_min;
+  const char* env = std::getenv("PF_CHUNKS_PER_THREAD");
+  int64_t tile = tile_min * (env ? std::max(1, std::atoi(env)) : 1);
+  if ((h->N + tile - 1) / tile > MAXG) tile = (h->N + MAXG - 1) / MAXG;
+  tile = (tile + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
+  if (tile > h->N) tile = (h->N + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
+  if (tile > h->ops->tile_max) return false;
   h->tile = (int)tile;
   h->G = (int)((h->N + tile - 1) / tile);
+  return h->G <= MAXG;
 }
 
-size_t step_lds(const pf_handle* h, bool sys_gather) {
-  const size_t area = std::max<size_t>(sys_gather ? (size_t)h->tile : 0, (size_t)NWAVES * h->ops->rec_size);
-  return base_lds_bytes() + area * sizeof(double);
+// k_step LDS: base | tile CDF (doubles) + ancestor slots (ints) when gathering | epilogue record staging
+size_t step_lds(const pf_handle* h, bool gather) {
+  const size_t epi = (size_t)h->ops->rec_size * sizeof(double);
+  const size_t gat = gather ? (size_t)h->tile * (sizeof(double) + sizeof(int)) : 0;
+  return base_lds_bytes(h->G) + std::max(epi, gat);
 }
 
 template <typename T>
@@ -204,9 +205,8 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
   p.lw_out = h->lw[h->clw ^ 1];
   p.rec_in = h->rec[h->crec];
   p.rec_out = h->rec[h->crec ^ 1];
-  const bool sys_gather = p.allow_gather && h->method == 0;
   dim3 grid((unsigned)h->G, (unsigned)h->R);
-  HIPCHK(h->ops->step(p, grid, step_lds(h, sys_gather), h->stream));
+  HIPCHK(h->ops->step(p, grid, step_lds(h, p.allow_gather != 0), h->stream));
   if (writes_x) h->cx ^= 1;
   if (writes_lw) h->clw ^= 1;
   if (writes_rec) h->crec ^= 1;
@@ -217,7 +217,7 @@ pf_status launch_cdf(pf_handle* h, StepParams p) {
   p.rec_in = h->rec[h->crec];
   p.lw_in = h->lw[h->clw];
   dim3 grid((unsigned)h->G, (unsigned)h->R);
-  HIPCHK(h->ops->cdf(p, h->cdf, grid, base_lds_bytes() + (size_t)h->tile * sizeof(double), h->stream));
+  HIPCHK(h->ops->cdf(p, h->cdf, grid, base_lds_bytes(h->G) + (size_t)h->tile * sizeof(double), h->stream));
   return PF_OK;
 }
 
@@ -345,6 +345,8 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
       P[lay_LR + i * nz + j] = L[i * nz + j];
       if (i != j && L[i * nz + j] != 0.0) r_diag = 0;
     }
+  const int lay_ILR = lay_EX + 2 + 2 * nz;
+  for (int i = 0; i < nz; ++i) P[lay_ILR + i] = 1.0 / L[i * nz + i];
   // predict: chol(Q), fallback chol(Q + 1e-10 I)  (particle_filter.py:232-235)
   bool qok = cholesky(m->Q, nx, 0.0, L) || cholesky(m->Q, nx, 1e-10, L);
   if (qok)
@@ -370,7 +372,11 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   h->r_diag = r_diag;
   h->chol_q_ok = qok;
   h->Pd = P;
-  choose_geometry(h);
+  if (!choose_geometry(h)) {
+    delete h;
+    return fail(PF_E_ARG, "n_particles too large for this model (max " +
+                              std::to_string((long long)MAXG * ops->tile_max) + ")");
+  }
   ops->prepare();
   auto cleanup = [&](pf_status st) {
     pf_destroy(h);
@@ -725,7 +731,7 @@ int32_t pf_weights_uniform(pf_handle* h) {
   int32_t all = 1;
   for (int r = 0; r < h->R; ++r) {
     double u = 0.0;
-    if (hipMemcpy(&u, h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3, sizeof(double),
+    if (hipMemcpy(&u, h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3 * (size_t)h->G, sizeof(double),
                   hipMemcpyDeviceToHost) != hipSuccess)
       return 0;
     all = all && (u != 0.0);
@@ -751,7 +757,7 @@ pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
   HIPCHK(hipMemcpyAsync(buf.data(), h->d_out, buf.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   std::vector<double> uni(h->R);
   for (int r = 0; r < h->R; ++r)
-    HIPCHK(hipMemcpyAsync(&uni[r], h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3, sizeof(double),
+    HIPCHK(hipMemcpyAsync(&uni[r], h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3 * (size_t)h->G, sizeof(double),
                           hipMemcpyDeviceToHost, h->stream));
   std::vector<double> lw;
   st = download_real(h, h->lw[h->clw], (size_t)h->R * h->Npad, lw);
@@ -787,15 +793,16 @@ pf_status pf_set_state(pf_handle* h, const double* particles, const double* weig
   if (st) return st;
   // records: one tile carrying S0 = 1 at m = 0 (so lse = 0), the rest empty; or uniform
   std::vector<double> rec((size_t)R * h->G * h->ops->rec_size, 0.0);
+  const size_t G = (size_t)h->G;
   for (int r = 0; r < R; ++r)
-    for (int k = 0; k < h->G; ++k) {
-      double* o = rec.data() + ((size_t)r * h->G + k) * h->ops->rec_size;
+    for (size_t k = 0; k < G; ++k) {
+      double* o = rec.data() + (size_t)r * G * h->ops->rec_size + k;  // SoA: field q at o[q*G]
       if (!weights) {
-        o[3] = 1.0;
+        o[3 * G] = 1.0;
       } else {
         o[0] = k == 0 ? 0.0 : -INFINITY;
-        o[1] = k == 0 ? 1.0 : 0.0;
-        o[2] = k == 0 ? 1.0 : 0.0;
+        o[1 * G] = k == 0 ? 1.0 : 0.0;
+        o[2 * G] = k == 0 ? 1.0 : 0.0;
       }
     }
   HIPCHK(hipMemcpy(h->rec[h->crec], rec.data(), rec.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -887,6 +894,14 @@ pf_status pf_resample_indices(int32_t device, int32_t method, const double* w, i
 
 void* pf_stream(pf_handle* h) { return h ? (void*)h->stream : nullptr; }
 
+#ifdef PF_STAMPS
+// diagnostic build only: copy out the per-workgroup phase stamps of the last k_step
+pf_status pf_debug_stamps(unsigned long long* out, int n) {
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pf_stamps), (size_t)n * sizeof(unsigned long long)));
+  return PF_OK;
+}
+#endif
+
 pf_status pf_synchronize(pf_handle* h) {
   if (!h) return fail(PF_E_ARG, "null handle");
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -897,7 +912,7 @@ pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds) {
   if (!h) return fail(PF_E_ARG, "null handle");
   if (G) *G = h->G;
   if (tile) *tile = h->tile;
-  if (lds) *lds = (int32_t)step_lds(h, h->method == 0);
+  if (lds) *lds = (int32_t)step_lds(h, true);
   return PF_OK;
 }
 

@@ -10,3 +10,10 @@ void register_sv_models() {
   register_both<3, 3, PF_TRANS_LINEAR, PF_OBS_EXP_HALF>();
 }
 }  // namespace pf
+
+#ifdef PF_STAMPS
+// diagnostic build only: this code object's copy of the stamp buffer
+extern "C" int pf_debug_stamps_sv(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pf::g_pf_stamps), (size_t)n * sizeof(unsigned long long));
+}
+#endif

@@ -2,12 +2,13 @@
 //
 // One launch of k_step = one pass over the particle set, fusing, in order:
 //   (0) prologue   every workgroup reduces the previous update's per-tile
-//                  partial records (tiny, L2-resident) to the global
-//                  log-normaliser, Neff, resample decision, systematic U and the
-//                  per-tile weight prefix.  All workgroups run the identical
-//                  fixed-order reduction, so they agree bit-for-bit and no
-//                  inter-workgroup communication is ever needed inside a launch;
-//                  workgroup 0 additionally writes that step's posterior outputs.
+//                  partial records (field-major, L2-resident) to the global log
+//                  normaliser, Neff, resample decision and — on resample steps —
+//                  the per-tile weight prefix.  All workgroups run the identical
+//                  fixed-order reduction (max first, then one exp per record, then
+//                  plain sums), so they agree bit-for-bit and no inter-workgroup
+//                  communication is needed inside a launch; workgroup 0 also
+//                  writes that step's posterior outputs.
 //   (1) gather     if the previous update decided to resample: each output slot
 //                  finds its ancestor (systematic: walk only the input tiles its
 //                  positions land in, scanning each tile's weights in LDS in fp64;
@@ -16,13 +17,18 @@
 //                  (particle_filter.py:188-220).
 //   (2) predict    x <- g(x, u) + chol(Q) n   (particle_filter.py:223-237)
 //   (3) update     l <- (l_prev - lse_prev) + loglik(z | x)  (particle_filter.py:239-263)
-//                  and the tile's online (max, sum e^(l-m), sum e^2(l-m), sum e^(l-m) x, ...)
+//                  and the tile's (max, sum e^(l-m), sum e^2(l-m), sum e^(l-m) x, ...)
 //                  partial record for the next launch's prologue.
+//
+// Occupancy is the design driver: a tile is one 4-particle chunk per thread
+// (16-byte vector loads/stores), several workgroups per CU, a rolled chunk loop
+// and no per-thread arrays, so that several waves per SIMD hide the latency of
+// the per-particle dependency chain (Philox -> Box-Muller -> g -> h -> weight).
 //
 // Layout in HBM (replicate-major, structure-of-arrays):
 //   x   [R][NX][Npad]  Real     particles (ping-pong pair)
 //   lw  [R][Npad]      Real     unnormalised log weights (ping-pong pair)
-//   rec [R][G][RS]     double   per-tile partial records (ping-pong pair)
+//   rec [R][F][G]      double   per-tile partial records, field-major (ping-pong pair)
 //   cdf [R][N]         double   materialised CDF (multinomial only)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -35,10 +41,26 @@ namespace pf {
 
 constexpr int BLOCK = 256;
 constexpr int NWAVES = BLOCK / 64;
-constexpr int MAXG = 1024;  // tiles per replicate (prologue holds 4 records per thread)
+constexpr int MAXG = 1024;         // tiles per replicate
+
+// Diagnostic phase stamps (PF_STAMPS builds only; never in the product library):
+// per workgroup, thread 0 records s_memrealtime (100 MHz) at phase boundaries.
+#ifdef PF_STAMPS
+constexpr int STAMP_SLOTS = 10;
+__device__ unsigned long long g_pf_stamps[4096 * STAMP_SLOTS];
+#define PF_STAMP(k)                                                                     \
+  do {                                                                                  \
+    if (stamp_on && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4096)            \
+      g_pf_stamps[blockIdx.x * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define PF_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
-// Partial record layout (doubles), one per (replicate, tile)
+// Partial record layout (doubles), field-major: rec[f * G + tile]
 // ---------------------------------------------------------------------------
 template <int NX>
 struct Rec {
@@ -47,8 +69,8 @@ struct Rec {
   static constexpr int M = 0;        // tile max of l (or -inf)
   static constexpr int S0 = 1;       // sum e^(l-m)
   static constexpr int S00 = 2;      // sum e^(2(l-m))
-  static constexpr int UNI = 3;      // 1.0: weights are uniform (after init / resample), head unused
-  static constexpr int CNT = 4;      // aux: number of freshly resampled particles in tile (0: aux invalid)
+  static constexpr int UNI = 3;      // 1.0: weights are uniform (after init / resample)
+  static constexpr int CNT = 4;      // aux: freshly resampled particles in tile (0: aux invalid)
   static constexpr int S1 = 5;       // NX   sum e^(l-m) x_d
   static constexpr int S2 = S1 + NX; // NC   sum e^(l-m) x_d x_e (d<=e)
   static constexpr int A1 = S2 + NC; // NX   aux: sum x_d of resampled particles
@@ -64,7 +86,8 @@ template <>
 __device__ __forceinline__ double exp_r<double>(double v) { return exp(v); }
 
 // ---------------------------------------------------------------------------
-// Wave / block collectives (fixed combination order -> deterministic)
+// Wave / block collectives (fixed combination order -> deterministic; an xor
+// butterfly gives every lane the bitwise-same result since + and max commute)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -90,19 +113,35 @@ __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
   return v;
 }
 
-// every thread returns the block total; `red` holds NWAVES doubles
-__device__ __forceinline__ double block_sum(double v, double* red) {
+// Block reductions (BS threads) over K values at once; `red` needs (BS/64)*K doubles.
+template <int K, int BS = BLOCK>
+__device__ __forceinline__ void block_sum_k(double (&v)[K], double* red) {
+  constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  v = wave_sum(v);
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  double s = red[0];
 #pragma unroll
-  for (int i = 1; i < NWAVES; ++i) s += red[i];
-  return s;
+  for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < K; ++i) red[w * K + i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double s = red[i];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) s += red[j * K + i];
+    v[i] = s;
+  }
 }
+template <int BS = BLOCK>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  double a[1] = {v};
+  block_sum_k<1, BS>(a, red);
+  return a[0];
+}
+template <int BS = BLOCK>
 __device__ __forceinline__ double block_max(double v, double* red) {
+  constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   v = wave_max(v);
   __syncthreads();
@@ -110,10 +149,12 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   __syncthreads();
   double s = red[0];
 #pragma unroll
-  for (int i = 1; i < NWAVES; ++i) s = fmax(s, red[i]);
+  for (int i = 1; i < NW; ++i) s = fmax(s, red[i]);
   return s;
 }
+template <int BS = BLOCK>
 __device__ __forceinline__ int block_min_i(int v, double* red) {
+  constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   v = wave_min_i(v);
   __syncthreads();
@@ -121,11 +162,13 @@ __device__ __forceinline__ int block_min_i(int v, double* red) {
   __syncthreads();
   int s = ((int*)red)[0];
 #pragma unroll
-  for (int i = 1; i < NWAVES; ++i) s = min(s, ((int*)red)[i]);
+  for (int i = 1; i < NW; ++i) s = min(s, ((int*)red)[i]);
   return s;
 }
 // exclusive block scan; returns this thread's offset, *total = block total
+template <int BS = BLOCK>
 __device__ __forceinline__ double block_excl_scan(double v, double* red, double* total) {
+  constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double incl = wave_incl_scan(v, lane);
   __syncthreads();
@@ -133,96 +176,13 @@ __device__ __forceinline__ double block_excl_scan(double v, double* red, double*
   __syncthreads();
   double off = 0.0, tot = 0.0;
 #pragma unroll
-  for (int i = 0; i < NWAVES; ++i) {
+  for (int i = 0; i < NW; ++i) {
     if (i < w) off += red[i];
     tot += red[i];
   }
   *total = tot;
   return off + incl - v;
 }
-
-// ---------------------------------------------------------------------------
-// Online weighted accumulator (per thread), combined across lanes/waves
-// ---------------------------------------------------------------------------
-template <typename Real, int NX>
-struct WAcc {
-  using RC = Rec<NX>;
-  double m;  // running max of l (exact value of some l)
-  double s0, s00;
-  double s1[NX];
-  double s2[RC::NC > 0 ? RC::NC : 1];
-
-  __device__ __forceinline__ void init() {
-    m = -INFINITY;
-    s0 = s00 = 0.0;
-#pragma unroll
-    for (int d = 0; d < NX; ++d) s1[d] = 0.0;
-#pragma unroll
-    for (int c = 0; c < RC::NC; ++c) s2[c] = 0.0;
-  }
-  __device__ __forceinline__ void scale(double f) {
-    s0 *= f;
-    s00 *= f * f;
-#pragma unroll
-    for (int d = 0; d < NX; ++d) s1[d] *= f;
-#pragma unroll
-    for (int c = 0; c < RC::NC; ++c) s2[c] *= f;
-  }
-  __device__ __forceinline__ void add(Real l, const Real* x) {
-    if (!(l > -INFINITY)) return;  // zero weight (l = -inf); NaN also skipped here, caught by neff
-    if ((double)l > m) {
-      if (m > -INFINITY) scale((double)exp_r<Real>((Real)(m - (double)l)));
-      m = (double)l;
-    }
-    const double e = (double)exp_r<Real>(l - (Real)m);
-    s0 += e;
-    s00 += e * e;
-#pragma unroll
-    for (int d = 0; d < NX; ++d) s1[d] += e * (double)x[d];
-    if constexpr (RC::COV) {
-      int c = 0;
-#pragma unroll
-      for (int d = 0; d < NX; ++d)
-#pragma unroll
-        for (int f = d; f < NX; ++f) s2[c++] += e * (double)x[d] * (double)x[f];
-    }
-  }
-  __device__ __forceinline__ void merge(double om, double os0, double os00, const double* os1,
-                                        const double* os2) {
-    if (!(om > -INFINITY)) return;
-    if (!(m > -INFINITY)) {
-      m = om;
-      s0 = os0;
-      s00 = os00;
-#pragma unroll
-      for (int d = 0; d < NX; ++d) s1[d] = os1[d];
-#pragma unroll
-      for (int c = 0; c < RC::NC; ++c) s2[c] = os2[c];
-      return;
-    }
-    const double M = fmax(m, om);
-    const double fa = exp(m - M), fb = exp(om - M);
-    s0 = s0 * fa + os0 * fb;
-    s00 = s00 * fa * fa + os00 * fb * fb;
-#pragma unroll
-    for (int d = 0; d < NX; ++d) s1[d] = s1[d] * fa + os1[d] * fb;
-#pragma unroll
-    for (int c = 0; c < RC::NC; ++c) s2[c] = s2[c] * fa + os2[c] * fb;
-    m = M;
-  }
-  __device__ __forceinline__ void wave_reduce() {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      double om = __shfl_xor(m, o), os0 = __shfl_xor(s0, o), os00 = __shfl_xor(s00, o);
-      double os1[NX], os2[RC::NC > 0 ? RC::NC : 1];
-#pragma unroll
-      for (int d = 0; d < NX; ++d) os1[d] = __shfl_xor(s1[d], o);
-#pragma unroll
-      for (int c = 0; c < RC::NC; ++c) os2[c] = __shfl_xor(s2[c], o);
-      merge(om, os0, os00, os1, os2);
-    }
-  }
-};
 
 // ---------------------------------------------------------------------------
 // Kernel parameters (by value)
@@ -261,67 +221,70 @@ struct StepParams {
 };
 
 struct Head {
-  double M, S, S2, lse, neff, U;
+  double M, S, S2, Sscan, lse, neff;
   int uniform, resample;
 };
 
-// Reduce the weight heads of rec (this replicate): M, S, S2, lse, Neff, decision,
-// and (if want_prefix) the normalised exclusive tile prefix P[0..G] into `Pl`.
-// Identical instruction stream in every workgroup -> identical results.
-__device__ __forceinline__ Head reduce_heads(const double* rec, int RS, int G, int64_t N, double thresh,
-                                             bool allow, double* red, double* Pl, bool want_prefix,
-                                             bool force = false) {
+// ---------------------------------------------------------------------------
+// Prologue: the summary of the previous launch's records.  Thread t owns the
+// contiguous records [t*RPT, t*RPT + RPT).  Max first, then per-record factors,
+// then plain sums: a short dependency chain with one parallel exp per record.
+// ---------------------------------------------------------------------------
+template <int NX, int BS>
+__device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, double thresh, bool allow, bool force,
+                                         bool want_prefix, double* red, double* Pl) {
+  using RC = Rec<NX>;
+  constexpr int RPT = MAXG / BS;  // records per thread
+  const int t = threadIdx.x;
+  const int k0 = t * RPT;
+  // one round of loads: the uniform flag and this thread's record heads
+  double mk[RPT], s0k[RPT], s00k[RPT];
+  const double uni = rec[RC::UNI * G];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int k = k0 + j;
+    const bool in = k < G;
+    mk[j] = in ? rec[RC::M * G + k] : -INFINITY;
+    s0k[j] = in ? rec[RC::S0 * G + k] : 0.0;
+    s00k[j] = in ? rec[RC::S00 * G + k] : 0.0;
+  }
   Head h;
-  h.uniform = rec[3] != 0.0;  // same in every record of a launch
+  h.uniform = uni != 0.0;  // a launch-wide property
   h.resample = 0;
-  h.U = 0.0;
   if (h.uniform) {
-    h.M = 0.0;
-    h.S = 1.0;
-    h.S2 = 1.0 / (double)N;
-    h.lse = 0.0;
-    h.neff = (double)N;
+    h.M = 0.0; h.S = h.S2 = h.Sscan = 1.0; h.lse = 0.0; h.neff = (double)N;
     return h;
   }
-  const int t = threadIdx.x;
-  double mk[4], s0k[4], s00k[4];
   double lmax = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = 4 * t + j;
-    if (k < G) {
-      mk[j] = rec[(int64_t)k * RS + 0];
-      s0k[j] = rec[(int64_t)k * RS + 1];
-      s00k[j] = rec[(int64_t)k * RS + 2];
-      if (s0k[j] > 0.0) lmax = fmax(lmax, mk[j]);
-    } else {
-      mk[j] = -INFINITY;
-      s0k[j] = s00k[j] = 0.0;
-    }
-  }
-  const double M = block_max(lmax, red);
-  double wk[4], v2 = 0.0, tsum = 0.0;
+  for (int j = 0; j < RPT; ++j)
+    if (s0k[j] > 0.0) lmax = fmax(lmax, mk[j]);
+  const double M = block_max<BS>(lmax, red);
+  double s[2] = {0.0, 0.0};
+  double wk[RPT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < RPT; ++j) {
     const double f = (s0k[j] > 0.0) ? exp(mk[j] - M) : 0.0;
     wk[j] = s0k[j] * f;
-    v2 += s00k[j] * f * f;
-    tsum += wk[j];
+    s[0] += wk[j];
+    s[1] += s00k[j] * f * f;
   }
-  double S;
-  const double off = block_excl_scan(tsum, red, &S);
-  const double S2 = block_sum(v2, red);
+  const double tsum = s[0];
+  block_sum_k<2, BS>(s, red);
   h.M = M;
-  h.S = S;
-  h.S2 = S2;
-  h.lse = M + log(S);
-  h.neff = (S * S) / S2;
+  h.S = s[0];
+  h.S2 = s[1];
+  h.Sscan = h.S;
+  h.lse = M + log(h.S);
+  h.neff = (h.S * h.S) / h.S2;
   h.resample = allow && (force || h.neff < thresh * (double)N);
-  if (want_prefix) {
-    double run = off;
+  if (want_prefix && h.resample) {  // normalised exclusive prefix of the tile weights
+    double S;
+    double run = block_excl_scan<BS>(tsum, red, &S);
+    h.Sscan = S;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = 4 * t + j;
+    for (int j = 0; j < RPT; ++j) {
+      const int k = k0 + j;
       if (k < G) Pl[k] = run / S;
       run += wk[j];
     }
@@ -331,84 +294,105 @@ __device__ __forceinline__ Head reduce_heads(const double* rec, int RS, int G, i
   return h;
 }
 
-// Block 0 only: posterior outputs of the update whose records are in `rec`
-// (weighted mean/cov, Neff, lse, decision) and of a resample whose fresh particles
-// were summarised in rec's aux part (uniform-weight mean/cov).
-template <int NX>
-__device__ void write_outputs(const StepParams& p, const double* rec, const Head& h, int r, int R,
+// Outputs of the update / resample summarised by `rec`: weighted mean/cov, Neff,
+// log normaliser, decision (out_step) and the uniform-weight mean/cov of freshly
+// resampled particles (out_post_step).  Field f of the output vector is reduced
+// by workgroup f mod nblk (spreads the work when NX is large).
+template <int NX, int BS>
+__device__ void write_outputs(const StepParams& p, const double* rec, const Head& h, int r, int R, int blk, int nblk,
                               double* red) {
   using RC = Rec<NX>;
   const int t = threadIdx.x;
-  if (p.out_step >= 0 && !h.uniform) {
+  const int G = p.G;
+  const bool pre = p.out_step >= 0 && !h.uniform;
+  const bool want_post = p.out_post_step >= 0;
+  if (!pre && !want_post) return;
+  if (pre && blk == 0 && t == 0) {
     const int64_t o = p.out_step * R + r;
-    for (int q = 0; q < NX + RC::NC; ++q) {
-      double acc = 0.0;
-      for (int k = 4 * t; k < 4 * t + 4 && k < p.G; ++k) {
-        const double s0 = rec[(int64_t)k * RC::SIZE + RC::S0];
-        if (s0 > 0.0) acc += rec[(int64_t)k * RC::SIZE + RC::S1 + q] * exp(rec[(int64_t)k * RC::SIZE] - h.M);
-      }
-      const double tot = block_sum(acc, red) / h.S;
-      if (t == 0) red[8 + q] = tot;  // stash E[x_d], E[x_d x_e]
-    }
-    __syncthreads();
-    if (t == 0) {
-      for (int d = 0; d < NX; ++d) p.o_mean[o * NX + d] = red[8 + d];
-      if (RC::COV && p.o_cov) {
-        int c = 0;
-        for (int d = 0; d < NX; ++d)
-          for (int f = d; f < NX; ++f, ++c) {
-            const double v = red[8 + NX + c] - red[8 + d] * red[8 + f];
-            p.o_cov[o * NX * NX + d * NX + f] = v;
-            p.o_cov[o * NX * NX + f * NX + d] = v;
-          }
-      }
-      p.o_neff[o] = h.neff;
-      p.o_lse[o] = h.lse;
-      p.o_flag[o] = h.resample;
-    }
-    __syncthreads();
+    p.o_neff[o] = h.neff;
+    p.o_lse[o] = h.lse;
+    p.o_flag[o] = h.resample;
   }
-  if (p.out_post_step >= 0) {
-    double cnt = 0.0;
-    for (int k = 4 * t; k < 4 * t + 4 && k < p.G; ++k) cnt += rec[(int64_t)k * RC::SIZE + RC::CNT];
-    cnt = block_sum(cnt, red);
-    if (cnt > 0.0) {
-      const int64_t o = p.out_post_step * R + r;
-      for (int q = 0; q < NX + RC::NC; ++q) {
-        double acc = 0.0;
-        for (int k = 4 * t; k < 4 * t + 4 && k < p.G; ++k) acc += rec[(int64_t)k * RC::SIZE + RC::A1 + q];
-        const double tot = block_sum(acc, red) / cnt;
-        if (t == 0) red[8 + q] = tot;
-      }
-      __syncthreads();
-      if (t == 0) {
-        for (int d = 0; d < NX; ++d) p.o_mean[o * NX + d] = red[8 + d];
-        if (RC::COV && p.o_cov) {
-          int c = 0;
-          for (int d = 0; d < NX; ++d)
-            for (int f = d; f < NX; ++f, ++c) {
-              const double v = red[8 + NX + c] - red[8 + d] * red[8 + f];
-              p.o_cov[o * NX * NX + d * NX + f] = v;
-              p.o_cov[o * NX * NX + f * NX + d] = v;
-            }
+  constexpr int NF = NX + RC::NC;  // means + (small NX) second moments
+  if constexpr (RC::COV) {
+    if (blk != 0) return;
+    double v[2 * NF + 1];
+#pragma unroll
+    for (int f = 0; f < 2 * NF + 1; ++f) v[f] = 0.0;
+    for (int k = t; k < G; k += BS) {
+      if (pre) {
+        const double s0 = rec[RC::S0 * G + k];
+        if (s0 > 0.0) {
+          const double fk = exp(rec[RC::M * G + k] - h.M);
+#pragma unroll
+          for (int f = 0; f < NF; ++f) v[f] += rec[(RC::S1 + f) * G + k] * fk;
         }
       }
-      __syncthreads();
+      if (want_post) {
+        v[2 * NF] += rec[RC::CNT * G + k];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) v[NF + f] += rec[(RC::A1 + f) * G + k];
+      }
+    }
+    block_sum_k<2 * NF + 1, BS>(v, red);
+    if (t != 0) return;
+    const double cnt = v[2 * NF];
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 0 ? !pre : !(want_post && cnt > 0.0)) continue;
+      const int64_t o = (pass == 0 ? p.out_step : p.out_post_step) * R + r;
+      const double* m = v + pass * NF;
+      const double den = pass == 0 ? h.S : cnt;
+      for (int d = 0; d < NX; ++d) p.o_mean[o * NX + d] = m[d] / den;
+      if (p.o_cov) {
+        int c = 0;
+        for (int d = 0; d < NX; ++d)
+          for (int e = d; e < NX; ++e, ++c) {
+            const double val = m[NX + c] / den - (m[d] / den) * (m[e] / den);
+            p.o_cov[o * NX * NX + d * NX + e] = val;
+            p.o_cov[o * NX * NX + e * NX + d] = val;
+          }
+      }
+    }
+  } else {
+    double cnt = 0.0;
+    if (want_post) {
+      for (int k = t; k < G; k += BS) cnt += rec[RC::CNT * G + k];
+      cnt = block_sum<BS>(cnt, red);
+    }
+    const bool post = want_post && cnt > 0.0;
+    for (int f = blk; f < 2 * NX; f += nblk) {
+      const bool is_post = f >= NX;
+      if (is_post ? !post : !pre) continue;
+      const int d = is_post ? f - NX : f;
+      double acc = 0.0;
+      for (int k = t; k < G; k += BS) {
+        if (is_post) {
+          acc += rec[(RC::A1 + d) * G + k];
+        } else {
+          const double s0 = rec[RC::S0 * G + k];
+          if (s0 > 0.0) acc += rec[(RC::S1 + d) * G + k] * exp(rec[RC::M * G + k] - h.M);
+        }
+      }
+      acc = block_sum<BS>(acc, red);
+      if (t == 0) {
+        const int64_t o = (is_post ? p.out_post_step : p.out_step) * R + r;
+        p.o_mean[o * NX + d] = acc / (is_post ? cnt : h.S);
+      }
     }
   }
 }
 
-// Build the global CDF values of input tile k in LDS:
+// Global CDF values of input tile k, in LDS:
 //   cdf[j] = P_k + (e^(m_k - M) / S) * sum_{j' <= j} e^(l_j' - m_k)
-// (the same per-element weights the update's partial records summed).
-template <typename Real>
-__device__ __forceinline__ int tile_cdf(const Real* __restrict__ lw, int64_t N, int tile, int k,
-                                        double mk, const Head& h, const double* Pl, double* cdf,
-                                        double* red) {
+// (the same per-element weights the update's records summed).
+template <typename Real, int NX, int BS>
+__device__ __forceinline__ int tile_cdf(const Real* __restrict__ lw, const double* rec, int G, int64_t N, int tile,
+                                        int k, const Head& h, const double* Pl, double* cdf, double* red) {
   const int64_t s = (int64_t)k * tile;
   const int len = (int)min((int64_t)tile, N - s);
-  const int per = (len + BLOCK - 1) / BLOCK;
+  const int per = (len + BS - 1) / BS;
   const int j0 = threadIdx.x * per;
+  const double mk = rec[Rec<NX>::M * G + k];
   const Real m = (Real)mk;
   double acc = 0.0;
   for (int j = j0; j < j0 + per && j < len; ++j) {
@@ -416,8 +400,8 @@ __device__ __forceinline__ int tile_cdf(const Real* __restrict__ lw, int64_t N, 
     acc += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
   }
   double tot;
-  double off = block_excl_scan(acc, red, &tot);
-  const double c = exp(mk - h.M) / h.S;
+  double off = block_excl_scan<BS>(acc, red, &tot);
+  const double c = (mk > -INFINITY) ? exp(mk - h.M) / h.Sscan : 0.0;
   const double base = Pl[k];
   for (int j = j0; j < j0 + per && j < len; ++j) {
     const Real l = lw[s + j];
@@ -437,8 +421,8 @@ __device__ __forceinline__ int lds_upper(const double* cdf, int len, double pos)
   }
   return lo < len ? lo : len - 1;
 }
+// first k with pos < P[k+1] (the tile whose CDF range holds pos); G-1 if none
 __device__ __forceinline__ int prefix_tile(const double* Pl, int G, double pos) {
-  // first k with pos < P[k+1]
   int lo = 0, hi = G;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -447,13 +431,16 @@ __device__ __forceinline__ int prefix_tile(const double* Pl, int G, double pos) 
   return lo < G ? lo : G - 1;
 }
 
-template <int NX>
+// ---------------------------------------------------------------------------
+// Normals
+// ---------------------------------------------------------------------------
+// NX normals of particle i (flat indices i*NX .. i*NX+NX-1) from Philox, or replay
+template <int NX, typename Real>
 __device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t lrep, uint32_t rep, uint32_t ep,
-                                             uint32_t stream, const double* replay, int64_t N,
-                                             float* n) {
+                                             uint32_t stream, const double* replay, int64_t N, Real* n) {
   if (replay) {
 #pragma unroll
-    for (int d = 0; d < NX; ++d) n[d] = (float)replay[((int64_t)lrep * N + i) * NX + d];
+    for (int d = 0; d < NX; ++d) n[d] = (Real)replay[((int64_t)lrep * N + i) * NX + d];
     return;
   }
   const int64_t f0 = i * NX, f1 = f0 + NX - 1;
@@ -462,7 +449,7 @@ __device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t 
   for (int gg = 0; gg < GMAX; ++gg) {
     const int64_t g = (f0 >> 2) + gg;
     if (g > (f1 >> 2)) break;
-    const Normal4<float> q = normal4<float>(seed, (uint32_t)g, rep, ep, stream);
+    const Normal4<Real> q = normal4<Real>(seed, (uint32_t)g, rep, ep, stream);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int64_t f = 4 * g + e;
@@ -470,56 +457,10 @@ __device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t 
     }
   }
 }
-template <int NX>
-__device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t lrep, uint32_t rep, uint32_t ep,
-                                             uint32_t stream, const double* replay, int64_t N,
-                                             double* n) {
-  if (replay) {
-#pragma unroll
-    for (int d = 0; d < NX; ++d) n[d] = replay[((int64_t)lrep * N + i) * NX + d];
-    return;
-  }
-  const int64_t f0 = i * NX, f1 = f0 + NX - 1;
-  constexpr int GMAX = (NX % 4 == 0) ? NX / 4 : NX / 4 + 2;
-#pragma unroll
-  for (int gg = 0; gg < GMAX; ++gg) {
-    const int64_t g = (f0 >> 2) + gg;
-    if (g > (f1 >> 2)) break;
-    const Normal4<double> q = normal4<double>(seed, (uint32_t)g, rep, ep, stream);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t f = 4 * g + e;
-      if (f >= f0 && f <= f1) n[f - f0] = q.v[e];
-    }
-  }
-}
-
-// 16-byte (fp32) / 2x16-byte (fp64) vector moves of 4 consecutive slots
-template <typename Real>
-__device__ __forceinline__ void load4(const Real* src, Real& a, Real& b, Real& c, Real& d) {
-  if constexpr (sizeof(Real) == 4) {
-    const float4 v = *(const float4*)src;
-    a = v.x; b = v.y; c = v.z; d = v.w;
-  } else {
-    const double2 v0 = *(const double2*)src;
-    const double2 v1 = *(const double2*)(src + 2);
-    a = v0.x; b = v0.y; c = v1.x; d = v1.y;
-  }
-}
-template <typename Real>
-__device__ __forceinline__ void store4(Real* dst, Real a, Real b, Real c, Real d) {
-  if constexpr (sizeof(Real) == 4) {
-    *(float4*)dst = make_float4(a, b, c, d);
-  } else {
-    *(double2*)dst = make_double2(a, b);
-    *(double2*)(dst + 2) = make_double2(c, d);
-  }
-}
-// normals of particles i0..i0+3 of a scalar state (flat indices i0..i0+3 = one group)
+// normals of scalar particles i0..i0+3 (flat indices i0..i0+3 = one Philox group)
 template <typename Real>
 __device__ __forceinline__ void chunk_normals4(uint64_t seed, int64_t i0, uint32_t lrep, uint32_t rep, uint32_t ep,
-                                               uint32_t stream, const double* replay, int64_t N,
-                                               Real* n) {
+                                               uint32_t stream, const double* replay, int64_t N, Real* n) {
   if (replay) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) n[e] = (i0 + e < N) ? (Real)replay[(int64_t)lrep * N + i0 + e] : Real(0);
@@ -530,29 +471,146 @@ __device__ __forceinline__ void chunk_normals4(uint64_t seed, int64_t i0, uint32
   for (int e = 0; e < 4; ++e) n[e] = q.v[e];
 }
 
+// 16-byte (fp32) / 2x16-byte (fp64) vector moves of 4 consecutive slots
+template <typename Real>
+__device__ __forceinline__ void load4(const Real* src, Real* v) {
+  if constexpr (sizeof(Real) == 4) {
+    const float4 a = *(const float4*)src;
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    const double2 a = *(const double2*)src;
+    const double2 b = *(const double2*)(src + 2);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+}
+template <typename Real>
+__device__ __forceinline__ void store4(Real* dst, const Real* v) {
+  if constexpr (sizeof(Real) == 4) {
+    *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    *(double2*)dst = make_double2(v[0], v[1]);
+    *(double2*)(dst + 2) = make_double2(v[2], v[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-thread weighted accumulator: running max + scaled sums (online, per thread
+// only a few particles), merged max-first across lanes and waves.
+// ---------------------------------------------------------------------------
+template <typename Real, int NX>
+struct WAcc {
+  using RC = Rec<NX>;
+  static constexpr int NS = 2 + NX + RC::NC;  // s0, s00, s1[NX], s2[NC]
+  // a thread sums only a few particles: accumulate in the engine precision,
+  // combine across lanes and waves in fp64
+  Real m;
+  Real s[NS];
+
+  __device__ __forceinline__ void init() {
+    m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s[i] = Real(0);
+  }
+  __device__ __forceinline__ void add(Real l, const Real* x) {
+    if (!(l > -INFINITY)) return;  // zero weight (l = -inf); NaN also skipped
+    if (l > m) {
+      if (m > -INFINITY) {
+        const Real f = exp_r<Real>(m - l);
+        s[0] *= f;
+        s[1] *= f * f;
+#pragma unroll
+        for (int i = 2; i < NS; ++i) s[i] *= f;
+      }
+      m = l;
+    }
+    const Real e = exp_r<Real>(l - m);
+    s[0] += e;
+    s[1] += e * e;
+#pragma unroll
+    for (int d = 0; d < NX; ++d) s[2 + d] += e * x[d];
+    if constexpr (RC::COV) {
+      int c = 2 + NX;
+#pragma unroll
+      for (int d = 0; d < NX; ++d)
+#pragma unroll
+        for (int f = d; f < NX; ++f) s[c++] += e * x[d] * x[f];
+    }
+  }
+  // Block merge (max first): result (m, s...) in out[0..NS] of thread 0 only.
+  // red >= (BS/64)*(NS+1) doubles.
+  template <int BS>
+  __device__ __forceinline__ void block_merge(double* red, double* out) {
+    constexpr int NW = BS / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const double md = (double)m;
+    const double Mw = wave_max(md);
+    const double f = (md > -INFINITY) ? exp(md - Mw) : 0.0;
+    double v[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) v[i] = wave_sum((double)s[i] * (i == 1 ? f * f : f));
+    __syncthreads();
+    if (lane == 0) {
+      red[w * (NS + 1)] = Mw;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) red[w * (NS + 1) + 1 + i] = v[i];
+    }
+    __syncthreads();
+    if (w != 0) return;
+    // wave 0: lane j < NW holds wave j's partial; one exp per lane, then a shuffle sum
+    const double mj = lane < NW ? red[lane * (NS + 1)] : -INFINITY;
+    const double M = wave_max(mj);
+    const double fj = (mj > -INFINITY) ? exp(mj - M) : 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const double vi = lane < NW ? red[lane * (NS + 1) + 1 + i] * (i == 1 ? fj * fj : fj) : 0.0;
+      out[1 + i] = wave_sum(vi);
+    }
+    out[0] = M;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // The fused step kernel
 // ---------------------------------------------------------------------------
 // Work split: workgroup (b, r) owns particle slots [b*tile, (b+1)*tile) of
 // replicate r.  A thread owns "chunks" of CH consecutive slots (CH = 4 for the
-// scalar state so x/lw move as 16-byte vectors), at most MAXC chunks.
+// scalar state so x / lw move as 16-byte vectors): chunk c = t, t+BLOCK, ...
+#ifndef PF_SMALL_BS
+#define PF_SMALL_BS 256
+#endif
+template <int NX>
+constexpr int step_bs = (NX == 1) ? PF_SMALL_BS : 256;
+
 template <typename Real, int NX, int NZ, int TK, int OK>
 struct StepTraits {
   static constexpr int CH = (NX == 1) ? 4 : 1;
-  static constexpr int MAXC = (NX == 1) ? 8 : 4;
-  static constexpr int TILE_MAX = BLOCK * CH * MAXC;
+  // Workgroup size: PF_SMALL_BS for the small-state models (bigger workgroups ->
+  // fewer tiles -> less O(tiles^2) prologue redundancy, but a lower VGPR cap);
+  // register-heavy large-state models (L96, MAT) keep 256.
+  static constexpr int BS = step_bs<NX>;
+  static constexpr int TILE_MAX = BS * CH * 16;  // at most 16 chunks per thread
 };
 
+// LDS carve (doubles): [0, LDS_RED) scratch | Pl[G+1] | tile area (cdf doubles + anc ints, or
+// the staged epilogue record)
+constexpr int LDS_RED = 512;
+constexpr int LDS_PL = LDS_RED;
+__host__ __device__ constexpr int lds_tile(int G) { return LDS_PL + ((G + 8) & ~7); }
+
 template <typename Real, int NX, int NZ, int TK, int OK>
-__global__ void __launch_bounds__(BLOCK) k_step(StepParams p) {
+__global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
-  using TR = StepTraits<Real, NX, NZ, TK, OK>;
-  constexpr int CH = TR::CH, MAXC = TR::MAXC;
+  using WA = WAcc<Real, NX>;
+  constexpr int CH = StepTraits<Real, NX, NZ, TK, OK>::CH;
+  constexpr int BS = StepTraits<Real, NX, NZ, TK, OK>::BS;
+  static_assert((BS / 64) * (WA::NS + 1) <= LDS_RED, "scratch too small");
+  static_assert((BS / 64) * (2 * (NX + Rec<NX>::NC) + 1) <= LDS_RED, "scratch too small");
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* red = smem;                   // 64 doubles scratch
-  double* Pl = smem + 64;               // G + 1 prefix
-  double* cdf = smem + 64 + MAXG + 8;   // tile doubles
+  double* red = smem;
+  double* Pl = smem + LDS_PL;
+  double* cdf = smem + lds_tile(p.G);
+  int* anc_l = (int*)(cdf + p.tile);
 
   const int b = blockIdx.x, r = blockIdx.y, R = gridDim.y;
   const int t = threadIdx.x;
@@ -561,191 +619,253 @@ __global__ void __launch_bounds__(BLOCK) k_step(StepParams p) {
   Real* x_out = (Real*)p.x_out + (int64_t)r * NX * p.Npad;
   const Real* lw_in = (const Real*)p.lw_in + (int64_t)r * p.Npad;
   Real* lw_out = (Real*)p.lw_out + (int64_t)r * p.Npad;
-  const double* rec_in = p.rec_in + (int64_t)r * p.G * RC::SIZE;
+  const double* rec_in = p.rec_in + (int64_t)r * RC::SIZE * p.G;
   const int64_t o0 = (int64_t)b * p.tile;
   const int64_t o1 = min(o0 + (int64_t)p.tile, p.N);
   const int nchunks = (int)((o1 - o0 + CH - 1) / CH);
+  const uint32_t rep = (uint32_t)(r + p.rep_base);
+  const bool stamp_on = p.do_predict && p.do_update;  // stamps: fused steps only
+  (void)stamp_on;
+  PF_STAMP(0);
 
-  // ---- (0) prologue -------------------------------------------------------
-  const bool need_gather_info = p.allow_gather != 0;
-  Head h = reduce_heads(rec_in, RC::SIZE, p.G, p.N, p.thresh, p.allow_gather != 0, red, Pl,
-                        need_gather_info && p.method == 0, p.force_gather != 0);
-  if (b == 0) write_outputs<NX>(p, rec_in, h, r, R, red);
-  const bool gather = h.resample != 0;
-  if (gather && p.method == 0)
-    h.U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, (uint32_t)(r + p.rep_base), p.ep_resample);
-  const double lprev_uniform = -log((double)p.N);
-
-  // ---- (1) ancestors -----------------------------------------------------
-  int anc[MAXC][CH];
-  if (gather) {
-    if (p.method == 0) {
-      int kk[MAXC][CH];
-      int nextk = p.G;
-      for (int q = 0; q < MAXC; ++q) {
-        const int c = t + q * BLOCK;
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          kk[q][e] = p.G;
-          anc[q][e] = -1;
-          const int64_t i = o0 + (int64_t)c * CH + e;
-          if (c < nchunks && i < o1) {
-            const double pos = (h.U + (double)i) / (double)p.N;
-            kk[q][e] = prefix_tile(Pl, p.G, pos);
-            nextk = min(nextk, kk[q][e]);
-          }
-        }
-      }
-      int k = block_min_i(nextk, red);
-      while (k < p.G) {
-        const double mk = rec_in[(int64_t)k * RC::SIZE + RC::M];
-        const int len = tile_cdf<Real>(lw_in, p.N, p.tile, k, mk, h, Pl, cdf, red);
-        nextk = p.G;
-        for (int q = 0; q < MAXC; ++q) {
-#pragma unroll
-          for (int e = 0; e < CH; ++e) {
-            if (kk[q][e] == k) {
-              const int64_t i = o0 + (int64_t)(t + q * BLOCK) * CH + e;
-              const double pos = (h.U + (double)i) / (double)p.N;
-              anc[q][e] = (int)((int64_t)k * p.tile + lds_upper(cdf, len, pos));
-              kk[q][e] = p.G;
-            } else if (kk[q][e] < p.G) {
-              nextk = min(nextk, kk[q][e]);
-            }
-          }
-        }
-        __syncthreads();  // cdf reused by the next tile
-        k = block_min_i(nextk, red);
-      }
-    } else {  // multinomial: binary search in the materialised CDF (cdf /= cdf[-1])
-      const double* C = p.cdf + (int64_t)r * p.N;
-      const double last = C[p.N - 1];
-      for (int q = 0; q < MAXC; ++q) {
-        const int c = t + q * BLOCK;
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          const int64_t i = o0 + (int64_t)c * CH + e;
-          anc[q][e] = -1;
-          if (c < nchunks && i < o1) {
-            const double uu = p.rp_unif ? p.rp_unif[(int64_t)r * p.N + i]
-                                        : uniform53(p.seed, (uint32_t)i, (uint32_t)(r + p.rep_base), p.ep_resample);
-            int64_t lo = 0, hi = p.N;
-            while (lo < hi) {
-              const int64_t mid = (lo + hi) >> 1;
-              if (uu < C[mid] / last) hi = mid; else lo = mid + 1;
-            }
-            anc[q][e] = (int)(lo < p.N ? lo : p.N - 1);
-          }
-        }
-      }
-    }
-  }
-
-  // ---- (2)+(3) per particle -----------------------------------------------
-  WAcc<Real, NX> acc;
-  acc.init();
-  double aux_cnt = 0.0, aux1[NX], aux2[RC::NC > 0 ? RC::NC : 1];
-#pragma unroll
-  for (int d = 0; d < NX; ++d) aux1[d] = 0.0;
-#pragma unroll
-  for (int c = 0; c < RC::NC; ++c) aux2[c] = 0.0;
-
+  // ---- (S) speculative first chunk --------------------------------------------
+  // Loads, normals, g and h of this thread's first chunk on the no-resample path do
+  // not depend on the prologue: computing them first overlaps the prologue's record
+  // loads.  On a resample step the chunk is redone from the gathered ancestors with
+  // the same (counter-based) normals.
+  constexpr bool PRE = NX <= 4;
+  constexpr int SC = PRE ? CH : 1;
+  Real sx[SC][NX], sl[SC], sll[SC], sn[SC][NX];
   Real z[NZ];
   if (p.do_update) {
 #pragma unroll
     for (int k = 0; k < NZ; ++k) z[k] = ((const Real*)p.z)[(int64_t)r * p.z_rs + k];
   }
   const Real* u = p.u ? (const Real*)p.u + (int64_t)r * p.u_rs : nullptr;
-  const double lse_prev = h.uniform ? 0.0 : h.lse;
+  if constexpr (PRE) {
+    if (t < nchunks) {
+      const int64_t i0 = o0 + (int64_t)t * CH;
+      if constexpr (CH == 4) {
+        Real v[4];
+        load4<Real>(x_in + i0, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sx[e][0] = v[e];
+        if (p.do_update) load4<Real>(lw_in + i0, sl);
+        if (p.do_predict) {
+          Real n4[4];
+          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sn[e][0] = n4[e];
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < NX; ++d) sx[0][d] = x_in[(int64_t)d * p.Npad + i0];
+        if (p.do_update) sl[0] = lw_in[i0];
+        if (p.do_predict) fill_normals<NX, Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, sn[0]);
+      }
+#pragma unroll
+      for (int e = 0; e < SC; ++e) {
+        if (i0 + e < o1) {
+          if (p.do_predict) {
+            M::transition(sx[e], P, u);
+            M::add_lower(sx[e], sn[e], P, M::L::LQ);
+          }
+          sll[e] = (p.do_update == 1) ? M::loglik(sx[e], z, P, p.r_diag != 0) : Real(0);
+        }
+      }
+    }
+  }
 
+  // ---- (0) prologue ---------------------------------------------------------
+  const Head h = prologue<NX, BS>(rec_in, p.G, p.N, p.thresh, p.allow_gather != 0, p.force_gather != 0,
+                              p.allow_gather != 0 && p.method == 0, red, Pl);
+  PF_STAMP(1);
+  write_outputs<NX, BS>(p, rec_in, h, r, R, b, p.G, red);
+  PF_STAMP(2);
+  const bool gather = h.resample != 0;
+  const double lprev_uniform = -log((double)p.N);
+
+  // ---- (1) ancestors of this thread's slots (thread-private LDS entries) ----
+  if (gather) {
+    if (p.method == 0) {
+      const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
+      int nextk = p.G;
+      for (int c = t; c < nchunks; c += BS) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+          const int64_t i = o0 + (int64_t)c * CH + e;
+          if (i < o1) {
+            const int k = prefix_tile(Pl, p.G, (U + (double)i) / (double)p.N);
+            anc_l[c * CH + e] = -1 - k;  // pending, in tile k
+            nextk = min(nextk, k);
+          }
+        }
+      }
+      int k = block_min_i<BS>(nextk, red);
+      while (k < p.G) {
+        const int len = tile_cdf<Real, NX, BS>(lw_in, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red);
+        nextk = p.G;
+        for (int c = t; c < nchunks; c += BS) {
+#pragma unroll
+          for (int e = 0; e < CH; ++e) {
+            const int64_t i = o0 + (int64_t)c * CH + e;
+            if (i < o1) {
+              const int a = anc_l[c * CH + e];
+              if (a == -1 - k) {
+                anc_l[c * CH + e] = (int)((int64_t)k * p.tile + lds_upper(cdf, len, (U + (double)i) / (double)p.N));
+              } else if (a < 0) {
+                nextk = min(nextk, -1 - a);
+              }
+            }
+          }
+        }
+        __syncthreads();  // the tile CDF is rebuilt for the next tile
+        k = block_min_i<BS>(nextk, red);
+      }
+    } else {  // multinomial: binary search of the materialised CDF (cdf /= cdf[-1])
+      const double* C = p.cdf + (int64_t)r * p.N;
+      const double last = C[p.N - 1];
+      for (int c = t; c < nchunks; c += BS) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+          const int64_t i = o0 + (int64_t)c * CH + e;
+          if (i < o1) {
+            const double uu = p.rp_unif ? p.rp_unif[(int64_t)r * p.N + i] : uniform53(p.seed, (uint32_t)i, rep, p.ep_resample);
+            int64_t lo = 0, hi = p.N;
+            while (lo < hi) {
+              const int64_t mid = (lo + hi) >> 1;
+              if (uu < C[mid] / last) hi = mid; else lo = mid + 1;
+            }
+            anc_l[c * CH + e] = (int)(lo < p.N ? lo : p.N - 1);
+          }
+        }
+      }
+    }
+  }
+  PF_STAMP(3);
+
+  // ---- (2)+(3) per chunk: [gather + jitter] -> [predict] -> [weight] -> store
+  WA acc;
+  acc.init();
+  constexpr int NA = 1 + NX + RC::NC;  // aux: cnt, sum x, sum x x^T
+  double aux[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) aux[i] = 0.0;
+  const double lse_prev = h.uniform ? 0.0 : h.lse;
+  const Real lse_r = (Real)lse_prev;
   const bool write_x = p.do_predict || p.allow_gather;  // gather launches always produce x_out
-  for (int q = 0; q < MAXC; ++q) {
-    const int c = t + q * BLOCK;
-    if (c >= nchunks) break;
+
+  for (int c = t; c < nchunks; c += BS) {
     const int64_t i0 = o0 + (int64_t)c * CH;
-    Real xs[CH][NX];
+    const bool first = PRE && c == t;
+    const bool spec = first && !gather;  // predicted x and loglik already computed
+    Real x[CH][NX];
     Real lp[CH];
-    // load (or gather) the particle(s) and their normalised previous log weight
+    Real ll[CH];
     if (gather) {
 #pragma unroll
       for (int e = 0; e < CH; ++e) {
-        const int a = anc[q][e] < 0 ? 0 : anc[q][e];
+        const int a = (i0 + e < o1) ? anc_l[c * CH + e] : 0;
 #pragma unroll
-        for (int d = 0; d < NX; ++d) xs[e][d] = x_in[(int64_t)d * p.Npad + a];
+        for (int d = 0; d < NX; ++d) x[e][d] = x_in[(int64_t)d * p.Npad + a];
         lp[e] = (Real)lprev_uniform;
       }
-    } else if constexpr (CH == 4) {
-      load4<Real>(x_in + i0, xs[0][0], xs[1][0], xs[2][0], xs[3][0]);
-      if (p.do_update) {
-        if (h.uniform) {
+    } else {
+      Real lraw[CH];
+      if (spec) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) lp[e] = (Real)lprev_uniform;
+        for (int e = 0; e < CH; ++e) {
+#pragma unroll
+          for (int d = 0; d < NX; ++d) x[e][d] = sx[SC == CH ? e : 0][d];
+          lraw[e] = sl[SC == CH ? e : 0];
+          ll[e] = sll[SC == CH ? e : 0];
+        }
+      } else if constexpr (CH == 4) {
+        Real v[4];
+        load4<Real>(x_in + i0, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e][0] = v[e];
+        if (p.do_update && !h.uniform) load4<Real>(lw_in + i0, lraw);
+      } else {
+#pragma unroll
+        for (int d = 0; d < NX; ++d) x[0][d] = x_in[(int64_t)d * p.Npad + i0];
+        if (p.do_update && !h.uniform) lraw[0] = lw_in[i0];
+      }
+      if (p.do_update) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e)
+          lp[e] = h.uniform ? (Real)lprev_uniform : lraw[e] - lse_r;
+      }
+    }
+
+    Real nj4[CH], np4[CH];
+    if constexpr (CH == 4) {  // one Philox call covers the chunk's 4 scalar particles
+      if (gather && p.regularize) chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4);
+      if (p.do_predict) {
+        if (first) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) np4[e] = sn[e][0];
         } else {
-          Real l0, l1, l2, l3;
-          load4<Real>(lw_in + i0, l0, l1, l2, l3);
-          lp[0] = (Real)((double)l0 - lse_prev); lp[1] = (Real)((double)l1 - lse_prev);
-          lp[2] = (Real)((double)l2 - lse_prev); lp[3] = (Real)((double)l3 - lse_prev);
+          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4);
         }
       }
-    } else {
-#pragma unroll
-      for (int d = 0; d < NX; ++d) xs[0][d] = x_in[(int64_t)d * p.Npad + i0];
-      if (p.do_update)
-        lp[0] = h.uniform ? (Real)lprev_uniform : (Real)((double)lw_in[i0] - lse_prev);
     }
-
-    // scalar state: one Philox call yields the normals of the chunk's 4 particles
-    Real nj4[CH], np4[CH];
-    if constexpr (CH == 4) {
-      if (gather && p.regularize) chunk_normals4<Real>(p.seed, i0, (uint32_t)r, (uint32_t)(r + p.rep_base), p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4);
-      if (p.do_predict) chunk_normals4<Real>(p.seed, i0, (uint32_t)r, (uint32_t)(r + p.rep_base), p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4);
-    }
-
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       const int64_t i = i0 + e;
-      const bool live = i < o1;
-      Real* x = xs[e];
-      if (gather && live) {
+      if (i >= o1) break;
+      Real* xe = x[e];
+      if (gather) {
         if (p.regularize) {
           Real n[NX];
           if constexpr (CH == 4) n[0] = nj4[e];
-          else fill_normals<NX>(p.seed, i, (uint32_t)r, (uint32_t)(r + p.rep_base), p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n);
-          M::add_lower(x, n, P, M::L::LJ);
+          else fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n);
+          M::add_lower(xe, n, P, M::L::LJ);
         }
-        aux_cnt += 1.0;
+        aux[0] += 1.0;
 #pragma unroll
-        for (int d = 0; d < NX; ++d) aux1[d] += (double)x[d];
+        for (int d = 0; d < NX; ++d) aux[1 + d] += (double)xe[d];
         if constexpr (RC::COV) {
-          int cc = 0;
+          int cc = 1 + NX;
 #pragma unroll
           for (int d = 0; d < NX; ++d)
 #pragma unroll
-            for (int f = d; f < NX; ++f) aux2[cc++] += (double)x[d] * (double)x[f];
+            for (int f = d; f < NX; ++f) aux[cc++] += (double)xe[d] * (double)xe[f];
         }
       }
-      if (p.do_predict && live) {
-        Real n[NX];
-        if constexpr (CH == 4) n[0] = np4[e];
-        else fill_normals<NX>(p.seed, i, (uint32_t)r, (uint32_t)(r + p.rep_base), p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n);
-        M::transition(x, P, u);
-        M::add_lower(x, n, P, M::L::LQ);
+      if (!spec) {
+        if (p.do_predict) {
+          Real n[NX];
+          if constexpr (CH == 4) {
+            n[0] = np4[e];
+          } else if (first) {
+#pragma unroll
+            for (int d = 0; d < NX; ++d) n[d] = sn[0][d];
+          } else {
+            fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n);
+          }
+          M::transition(xe, P, u);
+          M::add_lower(xe, n, P, M::L::LQ);
+        }
+        ll[e] = (p.do_update == 1) ? M::loglik(xe, z, P, p.r_diag != 0) : Real(0);
       }
-      if (p.do_update && live) {
-        if (p.do_update == 1) lp[e] = lp[e] + M::loglik(x, z, P, p.r_diag != 0);  // 2: reweigh only
-        acc.add(lp[e], x);
+      if (p.do_update) {
+        lp[e] = lp[e] + ll[e];  // log(w_prev) - quad/2  (do_update == 2: reweigh only, ll = 0)
+        acc.add(lp[e], xe);
       }
     }
-    // store
     if constexpr (CH == 4) {
       if (i0 + 3 < o1) {
-        if (write_x) store4<Real>(x_out + i0, xs[0][0], xs[1][0], xs[2][0], xs[3][0]);
-        if (p.do_update) store4<Real>(lw_out + i0, lp[0], lp[1], lp[2], lp[3]);
+        if (write_x) {
+          Real v[4] = {x[0][0], x[1][0], x[2][0], x[3][0]};
+          store4<Real>(x_out + i0, v);
+        }
+        if (p.do_update) store4<Real>(lw_out + i0, lp);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (i0 + e < o1) {
-            if (write_x) x_out[i0 + e] = xs[e][0];
+            if (write_x) x_out[i0 + e] = x[e][0];
             if (p.do_update) lw_out[i0 + e] = lp[e];
           }
         }
@@ -753,111 +873,79 @@ __global__ void __launch_bounds__(BLOCK) k_step(StepParams p) {
     } else {
       if (write_x)
 #pragma unroll
-        for (int d = 0; d < NX; ++d) x_out[(int64_t)d * p.Npad + i0] = xs[0][d];
+        for (int d = 0; d < NX; ++d) x_out[(int64_t)d * p.Npad + i0] = x[0][d];
       if (p.do_update) lw_out[i0] = lp[0];
     }
   }
+  PF_STAMP(4);
 
-  // ---- partial record ------------------------------------------------------
-  // (written only by launches that produce records: updates and gathers)
+  // ---- (4) this tile's partial record (field-major) --------------------------
   if (!(p.do_update || p.allow_gather)) return;
-  double* rec_out = p.rec_out + ((int64_t)r * p.G + b) * RC::SIZE;
-  double* wsm = smem + 64 + MAXG + 8;  // reuse cdf area: NWAVES x (RC::SIZE) doubles
-  __syncthreads();
+  double* rec_out = p.rec_out + (int64_t)r * RC::SIZE * p.G;
+  double* fin = cdf;  // staged record: RC::SIZE doubles (tile area is free again)
+  __syncthreads();    // all tile-CDF / ancestor reads are done
   if (p.do_update) {
-    acc.wave_reduce();
-    if ((t & 63) == 0) {
-      double* o = wsm + (t >> 6) * RC::SIZE;
-      o[RC::M] = acc.m; o[RC::S0] = acc.s0; o[RC::S00] = acc.s00;
-#pragma unroll
-      for (int d = 0; d < NX; ++d) o[RC::S1 + d] = acc.s1[d];
-#pragma unroll
-      for (int c = 0; c < RC::NC; ++c) o[RC::S2 + c] = acc.s2[c];
+    double w[1 + WA::NS];
+    acc.template block_merge<BS>(red, w);
+    if (t == 0) {
+      fin[RC::M] = w[0];
+      fin[RC::S0] = w[1];
+      fin[RC::S00] = w[2];
+      fin[RC::UNI] = 0.0;
+      for (int i = 0; i < NX + RC::NC; ++i) fin[RC::S1 + i] = w[3 + i];
+    }
+  } else if (t == 0) {
+    if (gather) {  // gather-only launch: weights become uniform
+      fin[RC::M] = 0.0; fin[RC::S0] = 0.0; fin[RC::S00] = 0.0; fin[RC::UNI] = 1.0;
+      for (int q = RC::S1; q < RC::A1; ++q) fin[q] = 0.0;
+    } else {  // gather-only launch that did not resample: carry the update's record over
+      for (int q = 0; q < RC::A1; ++q) fin[q] = rec_in[q * p.G + b];
     }
   }
-  // aux sums (plain adds)
   if (gather) {
-    aux_cnt = wave_sum(aux_cnt);
-#pragma unroll
-    for (int d = 0; d < NX; ++d) aux1[d] = wave_sum(aux1[d]);
-#pragma unroll
-    for (int c = 0; c < RC::NC; ++c) aux2[c] = wave_sum(aux2[c]);
-    if ((t & 63) == 0) {
-      double* o = wsm + (t >> 6) * RC::SIZE;
-      o[RC::CNT] = aux_cnt;
-#pragma unroll
-      for (int d = 0; d < NX; ++d) o[RC::A1 + d] = aux1[d];
-#pragma unroll
-      for (int c = 0; c < RC::NC; ++c) o[RC::A2 + c] = aux2[c];
+    block_sum_k<NA, BS>(aux, red);
+    if (t == 0) {
+      fin[RC::CNT] = aux[0];
+      for (int i = 0; i < NX + RC::NC; ++i) fin[RC::A1 + i] = aux[1 + i];
     }
+  } else if (t == 0) {
+    fin[RC::CNT] = 0.0;
+    for (int q = RC::A1; q < RC::SIZE; ++q) fin[q] = 0.0;
   }
   __syncthreads();
-  if (t == 0) {
-    if (p.do_update) {
-      WAcc<Real, NX> tot;
-      tot.init();
-      for (int w = 0; w < NWAVES; ++w) {
-        const double* o = wsm + w * RC::SIZE;
-        tot.merge(o[RC::M], o[RC::S0], o[RC::S00], o + RC::S1, o + RC::S2);
-      }
-      rec_out[RC::M] = tot.m; rec_out[RC::S0] = tot.s0; rec_out[RC::S00] = tot.s00;
-      rec_out[RC::UNI] = 0.0;
-      for (int d = 0; d < NX; ++d) rec_out[RC::S1 + d] = tot.s1[d];
-      for (int c = 0; c < RC::NC; ++c) rec_out[RC::S2 + c] = tot.s2[c];
-    } else if (gather) {  // gather-only launch: weights become uniform
-      rec_out[RC::M] = 0.0; rec_out[RC::S0] = 0.0; rec_out[RC::S00] = 0.0;
-      rec_out[RC::UNI] = 1.0;
-    } else {  // gather-only launch that did not resample: carry the update's head over
-      const double* ri = rec_in + (int64_t)b * RC::SIZE;
-      for (int q = 0; q < RC::A1; ++q) rec_out[q] = ri[q];
-    }
-    if (gather) {
-      double cnt = 0.0;
-      for (int w = 0; w < NWAVES; ++w) cnt += wsm[w * RC::SIZE + RC::CNT];
-      rec_out[RC::CNT] = cnt;
-      for (int q = 0; q < NX + RC::NC; ++q) {
-        double s = 0.0;
-        for (int w = 0; w < NWAVES; ++w) s += wsm[w * RC::SIZE + RC::A1 + q];
-        rec_out[RC::A1 + q] = s;
-      }
-    } else {
-      rec_out[RC::CNT] = 0.0;
-    }
-  }
+  PF_STAMP(5);
+  for (int q = t; q < RC::SIZE; q += BS) rec_out[q * p.G + b] = fin[q];
 }
 
 // ---------------------------------------------------------------------------
-// Finalize: posterior outputs of the records in rec (one workgroup per replicate)
+// Finalize: posterior outputs of the records in rec_in (one workgroup per replicate)
 // ---------------------------------------------------------------------------
-template <int NX>
-__global__ void __launch_bounds__(BLOCK) k_finalize(StepParams p) {
-  using RC = Rec<NX>;
+// (same block size and reduction tree as k_step's prologue -> bitwise the same decision)
+template <int NX, int BS>
+__global__ void __launch_bounds__(BS) k_finalize(StepParams p) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* red = smem;
   const int r = blockIdx.x, R = gridDim.x;
-  const double* rec = p.rec_in + (int64_t)r * p.G * RC::SIZE;
-  Head h = reduce_heads(rec, RC::SIZE, p.G, p.N, p.thresh, p.allow_gather != 0, red, nullptr, false);
-  write_outputs<NX>(p, rec, h, r, R, red);
+  const double* rec = p.rec_in + (int64_t)r * Rec<NX>::SIZE * p.G;
+  const Head h = prologue<NX, BS>(rec, p.G, p.N, p.thresh, p.allow_gather != 0, false, false, smem, nullptr);
+  write_outputs<NX, BS>(p, rec, h, r, R, 0, 1, smem);
 }
 
 // ---------------------------------------------------------------------------
 // Multinomial: materialise the CDF of the update in rec_in (if it resamples)
 // ---------------------------------------------------------------------------
-template <typename Real, int NX>
-__global__ void __launch_bounds__(BLOCK) k_cdf(StepParams p, double* cdf_out) {
-  using RC = Rec<NX>;
+template <typename Real, int NX, int BS>
+__global__ void __launch_bounds__(BS) k_cdf(StepParams p, double* cdf_out) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* red = smem;
-  double* Pl = smem + 64;
-  double* cdf = smem + 64 + MAXG + 8;
+  double* Pl = smem + LDS_PL;
+  double* cdf = smem + lds_tile(p.G);
   const int b = blockIdx.x, r = blockIdx.y;
-  const double* rec = p.rec_in + (int64_t)r * p.G * RC::SIZE;
-  Head h = reduce_heads(rec, RC::SIZE, p.G, p.N, p.thresh, true, red, Pl, true, p.force_gather != 0);
+  const double* rec = p.rec_in + (int64_t)r * Rec<NX>::SIZE * p.G;
+  const Head h = prologue<NX, BS>(rec, p.G, p.N, p.thresh, true, p.force_gather != 0, true, red, Pl);
   if (!h.resample) return;
   const Real* lw = (const Real*)p.lw_in + (int64_t)r * p.Npad;
-  const double mk = rec[(int64_t)b * RC::SIZE + RC::M];
-  const int len = tile_cdf<Real>(lw, p.N, p.tile, b, mk, h, Pl, cdf, red);
-  for (int j = threadIdx.x; j < len; j += BLOCK) cdf_out[(int64_t)r * p.N + (int64_t)b * p.tile + j] = cdf[j];
+  const int len = tile_cdf<Real, NX, BS>(lw, rec, p.G, p.N, p.tile, b, h, Pl, cdf, red);
+  for (int j = threadIdx.x; j < len; j += BS) cdf_out[(int64_t)r * p.N + (int64_t)b * p.tile + j] = cdf[j];
 }
 
 // ---------------------------------------------------------------------------
@@ -873,7 +961,7 @@ __global__ void __launch_bounds__(BLOCK) k_init(Real* x, double* rec, const Real
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i < N) {
     Real n[NX];
-    fill_normals<NX>(seed, i, (uint32_t)r, (uint32_t)(r + rep_base), epoch, STREAM_INIT, replay, N, n);
+    fill_normals<NX, Real>(seed, i, (uint32_t)r, (uint32_t)(r + rep_base), epoch, STREAM_INIT, replay, N, n);
     const Real* L = Lc + (int64_t)r * NX * NX;
 #pragma unroll
     for (int d = 0; d < NX; ++d) {
@@ -883,11 +971,11 @@ __global__ void __launch_bounds__(BLOCK) k_init(Real* x, double* rec, const Real
       x[((int64_t)r * NX + d) * Npad + i] = acc + mean[r * NX + d];
     }
   }
-  const int64_t k = i;  // one record per tile
+  const int64_t k = i;  // one record per tile (field q at [q*G + k])
   if (k < G) {
-    double* o = rec + ((int64_t)r * G + k) * RC::SIZE;
-    for (int q = 0; q < RC::SIZE; ++q) o[q] = 0.0;
-    o[RC::UNI] = 1.0;
+    double* o = rec + (int64_t)r * RC::SIZE * G;
+    for (int q = 0; q < RC::SIZE; ++q) o[(int64_t)q * G + k] = 0.0;
+    o[(int64_t)RC::UNI * G + k] = 1.0;
   }
 }
 
@@ -909,18 +997,17 @@ __global__ void __launch_bounds__(BLOCK) k_mom_mean(const Real* x, const Real* l
                                                     const double* lse, int64_t N, int64_t Npad, double* mean) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int d = blockIdx.x, r = blockIdx.y;
-  const bool uni = rec[(int64_t)r * G * RS + 3] != 0.0;
+  const bool uni = rec[(int64_t)r * G * RS + 3 * (int64_t)G] != 0.0;
   const Real* xr = x + ((int64_t)r * NX + d) * Npad;
   const Real* lr = lw + (int64_t)r * Npad;
-  double sw = 0.0, sx = 0.0;
+  double v[2] = {0.0, 0.0};
   for (int64_t i = threadIdx.x; i < N; i += BLOCK) {
     const double w = mom_weight<Real>(lr, i, uni, lse[r]);
-    sw += w;
-    sx += w * (double)xr[i];
+    v[0] += w;
+    v[1] += w * (double)xr[i];
   }
-  sw = block_sum(sw, smem);
-  sx = block_sum(sx, smem);
-  if (threadIdx.x == 0) mean[(int64_t)r * NX + d] = sx / sw;
+  block_sum_k<2>(v, smem);
+  if (threadIdx.x == 0) mean[(int64_t)r * NX + d] = v[1] / v[0];
 }
 
 template <typename Real, int NX>
@@ -930,22 +1017,21 @@ __global__ void __launch_bounds__(BLOCK) k_mom_cov(const Real* x, const Real* lw
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int d = blockIdx.x / NX, e = blockIdx.x % NX, r = blockIdx.y;
   if (e < d) return;
-  const bool uni = rec[(int64_t)r * G * RS + 3] != 0.0;
+  const bool uni = rec[(int64_t)r * G * RS + 3 * (int64_t)G] != 0.0;
   const Real* xd = x + ((int64_t)r * NX + d) * Npad;
   const Real* xe = x + ((int64_t)r * NX + e) * Npad;
   const Real* lr = lw + (int64_t)r * Npad;
   const double md = mean[(int64_t)r * NX + d], me = mean[(int64_t)r * NX + e];
-  double sw = 0.0, sc = 0.0;
+  double v[2] = {0.0, 0.0};
   for (int64_t i = threadIdx.x; i < N; i += BLOCK) {
     const double w = mom_weight<Real>(lr, i, uni, lse[r]);
-    sw += w;
-    sc += w * ((double)xd[i] - md) * ((double)xe[i] - me);
+    v[0] += w;
+    v[1] += w * ((double)xd[i] - md) * ((double)xe[i] - me);
   }
-  sw = block_sum(sw, smem);
-  sc = block_sum(sc, smem);
+  block_sum_k<2>(v, smem);
   if (threadIdx.x == 0) {
-    cov[(int64_t)r * NX * NX + d * NX + e] = sc / sw;
-    cov[(int64_t)r * NX * NX + e * NX + d] = sc / sw;
+    cov[(int64_t)r * NX * NX + d * NX + e] = v[1] / v[0];
+    cov[(int64_t)r * NX * NX + e * NX + d] = v[1] / v[0];
   }
 }
 

@@ -26,7 +26,8 @@ struct ParamLayout {
   static constexpr int C = H + NZ * NX;      // NZ     observation offset (LINEAR) / beta (EXP_HALF)
   static constexpr int LR = C + NZ;          // NZ*NZ  chol(R + 1e-12 I)
   static constexpr int EX = LR + NZ * NZ;    // model extras: L96 {F, dt}; ACOUSTIC {psi, d0, sx[NZ], sy[NZ]}
-  static constexpr int SIZE = EX + 2 + 2 * NZ;
+  static constexpr int ILR = EX + 2 + 2 * NZ; // NZ     1 / diag(LR) (fp32 engine multiplies)
+  static constexpr int SIZE = ILR + NZ;
 };
 
 template <typename Real, int NX, int NZ, int TK, int OK>
@@ -119,7 +120,10 @@ struct Model {
     if (r_diag) {
 #pragma unroll
       for (int k = 0; k < NZ; ++k) {
-        y[k] = (z[k] - zp[k]) / P[L::LR + k * NZ + k];
+        if constexpr (sizeof(Real) == 4)
+          y[k] = (z[k] - zp[k]) * P[L::ILR + k];  // fp32: reciprocal multiply
+        else
+          y[k] = (z[k] - zp[k]) / P[L::LR + k * NZ + k];  // fp64: the reference's division
         quad += y[k] * y[k];
       }
     } else {  // forward substitution with the lower-triangular LR

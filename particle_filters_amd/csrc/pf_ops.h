@@ -14,7 +14,7 @@ namespace pf {
 
 struct Ops {
   int nx, nz, tk, ok, prec;
-  int rec_size, ch, tile_max, psize;
+  int rec_size, ch, tile_max, tile_min, psize;
   hipError_t (*step)(const StepParams&, dim3, size_t, hipStream_t);
   hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
   hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
@@ -28,20 +28,21 @@ struct Ops {
 void register_ops(const Ops& o);
 const Ops* find_ops(int nx, int nz, int tk, int ok, int prec);
 
-inline size_t base_lds_bytes() { return (size_t)(64 + MAXG + 8) * sizeof(double); }
+inline size_t base_lds_bytes(int G) { return (size_t)lds_tile(G) * sizeof(double); }
 
 template <typename Real, int NX, int NZ, int TK, int OK>
 struct Launch {
+  static constexpr int BS = StepTraits<Real, NX, NZ, TK, OK>::BS;
   static hipError_t step(const StepParams& p, dim3 grid, size_t smem, hipStream_t s) {
-    hipLaunchKernelGGL((k_step<Real, NX, NZ, TK, OK>), grid, dim3(BLOCK), smem, s, p);
+    hipLaunchKernelGGL((k_step<Real, NX, NZ, TK, OK>), grid, dim3(BS), smem, s, p);
     return hipGetLastError();
   }
   static hipError_t finalize(const StepParams& p, int R, hipStream_t s) {
-    hipLaunchKernelGGL((k_finalize<NX>), dim3(R), dim3(BLOCK), 64 * sizeof(double), s, p);
+    hipLaunchKernelGGL((k_finalize<NX, BS>), dim3(R), dim3(BS), LDS_RED * sizeof(double), s, p);
     return hipGetLastError();
   }
   static hipError_t cdf(const StepParams& p, double* out, dim3 grid, size_t smem, hipStream_t s) {
-    hipLaunchKernelGGL((k_cdf<Real, NX>), grid, dim3(BLOCK), smem, s, p, out);
+    hipLaunchKernelGGL((k_cdf<Real, NX, BS>), grid, dim3(BS), smem, s, p, out);
     return hipGetLastError();
   }
   static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
@@ -68,6 +69,7 @@ struct Launch {
     o.rec_size = Rec<NX>::SIZE;
     o.ch = StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.tile_max = StepTraits<Real, NX, NZ, TK, OK>::TILE_MAX;
+    o.tile_min = BS * StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.psize = ParamLayout<NX, NZ>::SIZE;
     o.step = &step;
     o.finalize = &finalize;
@@ -81,7 +83,7 @@ struct Launch {
     // allow up to 160 KiB of dynamic LDS for the tile CDF
     (void)hipFuncSetAttribute((const void*)k_step<Real, NX, NZ, TK, OK>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_cdf<Real, NX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_cdf<Real, NX, BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
   }
 };
