@@ -14,11 +14,15 @@ RCCL all-gather of every replicate's posterior summaries (means, ESS, flags),
 bracketed by barrier + device synchronisation; the max over ranks is reported.
 
 Extra JSON fields:
-  roofline      dominant kernel k_step<f32, SV>: algorithmic bytes per launch
-                (N x 16 B: read x, lw; write x, lw) / its average device duration,
-                timed live with HIP events on the engine's stream; traffic = HBM
-                bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE
-                doubled per the gfx950 rule + WRITE_SIZE), or null.
+  roofline      dominant kernel k_step<f32, SV> (one launch = one filter step):
+                algorithmic bytes per launch (N x 16 B: read x, lw; write x, lw —
+                SURVEY.md 8(d)) / its average device duration, timed live with HIP
+                events recorded on the engine's own stream around the timed K-step
+                run (device time / K; the run's one tail launch is charged to the
+                steps, so this slightly overstates a launch); traffic = HBM bytes
+                per launch from the committed rocprofv3 PMC passes
+                (profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 rule
+                + WRITE_SIZE), or null.
   cpu_baseline  the reference CPU path (faithful per-particle restatement in
                 oracle/, bit-identical to the reference) timed on this host's cores
                 on a bounded sample of the same workload.
@@ -130,9 +134,14 @@ def main():
     ow, ot = outs(W), outs(K)
     gathered = [torch.zeros((K, 3), dtype=torch.float64, device=dev) for _ in range(world)]
 
+    engine_stream = torch.cuda.ExternalStream(lib.pf_stream(pf.handle), device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
     def job(dz, T, o):
         """One pass of the timed sequence: T filter steps + RCCL gather of the summaries."""
+        ev0.record(engine_stream)
         run(dz, T, o)
+        ev1.record(engine_stream)
         NV.check(lib.pf_synchronize(pf.handle))
         summary = torch.stack([o[0][:, 0], o[1][:, 0], o[2][:, 0].to(torch.float64)], dim=1)
         if summary.shape[0] < K:
@@ -154,6 +163,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    device_ms = ev0.elapsed_time(ev1)  # device time of the K-step run on the engine stream
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -164,13 +174,14 @@ def main():
     allm = torch.stack(gathered).cpu().numpy()  # [world][K][3]
     rmse = [float(np.sqrt(np.mean((allm[r, :, 0] - truth) ** 2))) for r in range(world)]
 
-    # live roofline of the dominant kernel (per-launch HIP events on the engine stream)
+    # live roofline of the dominant kernel: device time of the timed run / launches
+    avg_s = device_ms * 1e-3 / K
+    # per-launch spread (one event pair per launch; the events themselves add gaps)
     nprof = args.profile_launches
     dZp = torch.tensor(np.resize(Zall, nprof), dtype=torch.float32, device=dev).contiguous()
     ms = (NV.C.c_float * nprof)()
     NV.check(lib.pf_profile_steps(pf.handle, NV.C.c_void_p(dZp.data_ptr()), nprof, ms), "pf_profile_steps")
     durs = np.array(ms[:], dtype=float)[10:]  # drop the first launches (clock ramp)
-    avg_s = float(np.mean(durs)) * 1e-3
     alg_bytes = N_PARTICLES * 16.0
     achieved = alg_bytes / avg_s / 1e9
     traffic, traffic_src = pmc_traffic()
@@ -210,7 +221,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pf::k_step<float,1,1,LINEAR,LINEAR>",
                          "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_us": avg_s * 1e6,
-                         "launches_timed": int(len(durs)), "traffic_source": traffic_src},
+                         "launches_timed": K, "traffic_source": traffic_src,
+                         "event_per_launch_us": {"median": float(np.median(durs)) * 1e3,
+                                                 "p10": float(np.percentile(durs, 10)) * 1e3,
+                                                 "p90": float(np.percentile(durs, 90)) * 1e3}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -1,0 +1,124 @@
+"""CPU checks of the C-ABI boundary (no GPU, no compute calls).
+
+* libpf_hip.so loads and exports every function include/pf_engine.h declares,
+  and the ctypes binding (particle_filters_amd/_native.py) covers exactly that set;
+* host-only entry points (version, model registry, argument validation in
+  pf_create) answer without a device;
+* the status -> exception mapping mirrors the reference's error behaviour
+  (particle_filter.py:142,231,252 AssertionError; LinAlgError for non-PD).
+"""
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from particle_filters_amd import _native as NV
+from particle_filters_amd import models as M
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "pf_engine.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(pf_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_parses_all_entry_points():
+    names = header_functions()
+    assert len(names) >= 20
+    for must in ("pf_create", "pf_destroy", "pf_initialize", "pf_predict", "pf_update", "pf_resample",
+                 "pf_run", "pf_run_device", "pf_resample_indices", "pf_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(NV.LIB_PATH)
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared in pf_engine.h but not exported: {missing}"
+
+
+def test_binding_covers_header_exactly():
+    assert sorted(NV.SIGNATURES) == header_functions()
+    lib = NV.load()
+    for n in NV.SIGNATURES:
+        assert getattr(lib, n).argtypes is not None or NV.SIGNATURES[n][1] == []
+
+
+def test_exports_are_plain_c_symbols():
+    # extern "C": no C++ mangling on the ABI surface
+    lib = C.CDLL(NV.LIB_PATH)
+    for n in header_functions():
+        assert C.cast(getattr(lib, n), C.c_void_p).value
+
+
+def test_version_string():
+    v = NV.load().pf_version().decode()
+    assert re.search(r"\d+\.\d+", v) and "gfx950" in v, v
+
+
+def test_model_registry():
+    lib = NV.load()
+    # compiled instantiations (pf_inst_*.hip)
+    assert lib.pf_model_supported(1, 1, NV.PF_TRANS_LINEAR, NV.PF_OBS_LINEAR)
+    assert lib.pf_model_supported(1, 1, NV.PF_TRANS_LINEAR, NV.PF_OBS_EXP_HALF)
+    assert lib.pf_model_supported(3, 3, NV.PF_TRANS_LINEAR, NV.PF_OBS_EXP_HALF)
+    assert lib.pf_model_supported(40, 10, NV.PF_TRANS_L96, NV.PF_OBS_LINEAR)
+    assert lib.pf_model_supported(16, 25, NV.PF_TRANS_LINEAR, NV.PF_OBS_ACOUSTIC)
+    assert not lib.pf_model_supported(7, 3, NV.PF_TRANS_L96, NV.PF_OBS_ACOUSTIC)
+    assert M.supported(M.SVTransition(0.95), M.SVLogSqObservation(1.0))
+    assert M.supported(M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40))
+
+
+def _create(g, h, Q, R, **kw):
+    d, keep = M.describe(g, h, np.asarray(Q, float), np.asarray(R, float))
+    o = dict(n_particles=100, n_replicates=1, resample_method=0, resample_thresh=0.5, regularize=0,
+             precision=0, seed=1, device=0, replicate_base=0)
+    o.update(kw)
+    opts = NV.Opts(**o)
+    h_ = C.c_void_p()
+    st = NV.load().pf_create(C.byref(d), C.byref(opts), C.byref(h_))
+    return st, h_
+
+
+def test_create_rejects_bad_arguments_before_touching_a_device():
+    g, h = M.SVTransition(0.95), M.SVLogSqObservation(1.0)
+    st, hd = _create(g, h, [[0.04]], [[1.0]], n_particles=0)
+    assert st == NV.PF_E_ARG and not hd.value
+    assert "n_particles" in NV.load().pf_last_error().decode()
+    st, _ = _create(g, h, [[0.04]], [[1.0]], n_replicates=0)
+    assert st == NV.PF_E_ARG
+    st, _ = _create(g, h, [[0.04]], [[1.0]], precision=7)
+    assert st == NV.PF_E_ARG
+    with pytest.raises(ValueError):
+        NV.check(st)
+
+
+def test_create_unsupported_model():
+    A = np.eye(5)
+    st, _ = _create(M.LinearTransition(A), M.LinearObservation(np.ones((1, 5))), np.eye(5), [[1.0]])
+    assert st == NV.PF_E_UNSUPPORTED
+    with pytest.raises(NotImplementedError):
+        NV.check(st)
+
+
+def test_status_exception_mapping():
+    with pytest.raises(AssertionError, match="Filter not initialized."):
+        NV.check(NV.PF_E_NOT_INITIALIZED)
+    with pytest.raises(np.linalg.LinAlgError):
+        NV.check(NV.PF_E_NOT_PD)
+    with pytest.raises(NV.PFError):
+        NV.check(NV.PF_E_HIP)
+    NV.check(NV.PF_OK)
+
+
+def test_describe_validates_shapes():
+    with pytest.raises(ValueError):
+        M.describe(M.SVTransition(0.95), M.SVLogSqObservation(1.0), np.eye(2), np.eye(1))
+    with pytest.raises(ValueError):
+        M.describe(M.SVTransition(0.95), M.SVLogSqObservation(1.0), np.eye(1), np.eye(2))

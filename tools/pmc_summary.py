@@ -1,0 +1,47 @@
+"""Fold rocprofv3 PMC passes into profiles/pmc_traffic.json (read by bench.py).
+
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [KERNEL_SUBSTR] [OUT]
+
+FETCH_SIZE / WRITE_SIZE come from separate passes (they do not fit one TCC pass
+on gfx950).  Both are reported in KiB.  Per MI355X_MICROARCH.md (HBM section)
+FETCH_SIZE under-reports wide coalesced streaming reads by exactly 2x on gfx950,
+so it is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores.
+"""
+import csv
+import json
+import sys
+
+import numpy as np
+
+
+def per_launch(path, counter, kern):
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+         if kern in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not v:
+        raise SystemExit(f"no {counter} rows for kernel '{kern}' in {path}")
+    return np.array(v) * 1024.0  # KiB -> bytes
+
+
+def main():
+    fetch_csv, write_csv = sys.argv[1], sys.argv[2]
+    kern = sys.argv[3] if len(sys.argv) > 3 else "k_step<float, 1, 1, 0, 0>"
+    out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+    f = per_launch(fetch_csv, "FETCH_SIZE", kern)
+    w = per_launch(write_csv, "WRITE_SIZE", kern)
+    d = {
+        "kernel": kern,
+        "launches": [int(f.size), int(w.size)],
+        "fetch_bytes_raw_mean": float(f.mean()),
+        "fetch_bytes_mean_x2": float(2 * f.mean()),
+        "write_bytes_mean": float(w.mean()),
+        "bytes_per_launch": float(2 * f.mean() + w.mean()),
+        "source": f"rocprofv3 --pmc FETCH_SIZE ({fetch_csv}) and --pmc WRITE_SIZE ({write_csv}); "
+                  "KiB->B, FETCH doubled per the gfx950 rule",
+    }
+    with open(out, "w") as fh:
+        json.dump(d, fh, indent=1)
+    print(json.dumps(d, indent=1))
+
+
+if __name__ == "__main__":
+    main()
