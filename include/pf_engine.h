@@ -156,6 +156,11 @@ pf_status pf_resample_indices(int32_t device, int32_t method, const double* w, i
 void* pf_stream(pf_handle* h);
 pf_status pf_synchronize(pf_handle* h);
 pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* ms_out);
+/* 1 if the last pf_run / pf_run_device ran as the register-resident whole-run
+ * kernel (one launch for all T steps: scalar fp32 models, systematic resampling,
+ * grid co-resident), 0 if as the launch-per-step loop.  PF_RESIDENT=0 in the
+ * environment forces the launch-per-step loop. */
+int32_t pf_last_run_resident(pf_handle* h);
 /* Geometry of the step launch: tiles per replicate, tile size, dynamic LDS bytes. */
 pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds_bytes);
 

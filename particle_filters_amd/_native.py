@@ -80,6 +80,7 @@ SIGNATURES = {
     "pf_synchronize": (C.c_int32, [_vp]),
     "pf_profile_steps": (C.c_int32, [_vp, _vp, C.c_int64, C.POINTER(C.c_float)]),
     "pf_geometry": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "pf_last_run_resident": (C.c_int32, [_vp]),
 }
 
 _lib = None

@@ -121,6 +121,11 @@ class ParticleFilterBatch:
         N.check(N.load().pf_get_weights(self._h, N.dptr(out), None), "pf_get_weights")
         return out
 
+    @property
+    def last_run_resident(self) -> bool:
+        """True if the last run() executed as the register-resident whole-run kernel."""
+        return bool(N.load().pf_last_run_resident(self._h))
+
     def geometry(self):
         G, tile, lds = N.C.c_int32(), N.C.c_int32(), N.C.c_int32()
         N.check(N.load().pf_geometry(self._h, N.C.byref(G), N.C.byref(tile), N.C.byref(lds)), "pf_geometry")

@@ -111,6 +111,12 @@ struct pf_handle {
   uint32_t ep_res = 0;        // epoch reserved by the last update for its resample
   bool chol_q_ok = true;
   std::vector<double> Pd;     // params (double)
+  // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
+  unsigned long long* rsync = nullptr;
+  size_t rsync_bytes = 0;
+  bool res_unchecked = false;  // a resident launch whose timeout word is not yet read
+  int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
+  bool last_resident = false;  // the last pf_run_device ran k_resident
 };
 
 namespace {
@@ -281,6 +287,99 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
   return PF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident whole-run path (pf_resident.h).  Used by pf_run_device when
+// the model has a resident kernel (scalar fp32), systematic resampling, the
+// default k_step geometry and a grid that fits co-resident on the device;
+// otherwise *used stays false and the caller runs the launch-per-step loop.
+// PF_RESIDENT=0 disables it (A/B comparisons).
+// ---------------------------------------------------------------------------
+pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t fo, double* dm,
+                       double* dc, double* dn, int32_t* df, double* dl, bool* used) {
+  *used = false;
+  const char* env = std::getenv("PF_RESIDENT");
+  if (env && std::atoi(env) == 0) return PF_OK;
+  if (!h->ops->resident || h->method != 0 || !(h->tile == 1024 || h->N <= 1024) || T <= 0) return PF_OK;
+  const int G = (int)((h->N + RTILE - 1) / RTILE);
+  if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
+  const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
+  const size_t bytes = (gran_n + 2 * flag_n + 2) * sizeof(unsigned long long);
+  if (h->rsync_bytes < bytes) {
+    if (h->rsync) HIPCHK(hipFree(h->rsync));
+    h->rsync = nullptr;
+    h->rsync_bytes = 0;
+    HIPCHK(hipMalloc((void**)&h->rsync, bytes));
+    h->rsync_bytes = bytes;
+  }
+  if (h->pending) {  // a decision taken before this run is applied first (gather-only launch)
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  HIPCHK(hipMemsetAsync(h->rsync, 0, bytes, h->stream));
+  ResParams q;
+  std::memset(&q, 0, sizeof(q));
+  q.x_in = (const float*)h->x[h->cx];
+  q.lw_in = (const float*)h->lw[h->clw];
+  q.rec_in = h->rec[h->crec];
+  q.x_fin = (float*)h->x[h->cx];    // in place: every thread rewrites only its own slots
+  q.lw_fin = (float*)h->lw[h->clw];
+  q.rec_fin = h->rec[h->crec ^ 1];
+  q.xg = (float*)h->x[h->cx ^ 1];
+  q.lg = (float*)h->lw[h->clw ^ 1];
+  q.gran = h->rsync;
+  q.sflag = h->rsync + gran_n;
+  q.tsum = (double*)(h->rsync + gran_n + flag_n);
+  q.err = (unsigned int*)(h->rsync + gran_n + 2 * flag_n);
+  q.P = h->P;
+  q.z = (const float*)dZ;
+  q.u = (const float*)dU;
+  q.o_mean = dm;
+  q.o_cov = dc;
+  q.o_neff = dn;
+  q.o_lse = dl;
+  q.o_flag = df;
+  q.N = h->N;
+  q.Npad = h->Npad;
+  q.T = T;
+  q.G = G;
+  q.Gk = h->G;
+  q.tile_k = h->tile;
+  q.seed = h->seed;
+  q.ep0 = h->epoch;
+  q.first_update_only = fo ? 1 : 0;
+  q.thresh = h->thresh;
+  q.regularize = h->regularize;
+  q.r_diag = h->r_diag;
+  q.rep_base = h->rep_base;
+  const hipError_t e = h->ops->resident(q, G, h->R, h->stream);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    return PF_OK;  // not co-resident here: launch-per-step path
+  }
+  if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
+  const int k = fo ? 1 : 0;
+  h->epoch = q.ep0 + (uint32_t)(2 * T) - k;
+  h->ep_res = h->epoch - 1;
+  h->pending = false;
+  h->crec ^= 1;
+  h->res_unchecked = true;
+  h->resident_runs++;
+  h->last_resident = true;
+  *used = true;
+  return PF_OK;
+}
+
+// After a stream sync: a resident launch that timed out in a hand-off is an error.
+pf_status check_resident(pf_handle* h) {
+  if (!h->res_unchecked) return PF_OK;
+  h->res_unchecked = false;
+  const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
+  unsigned int err = 0;
+  HIPCHK(hipMemcpy(&err, (const void*)(h->rsync + gran_n + 2 * flag_n), sizeof(err), hipMemcpyDeviceToHost));
+  if (err) return fail(PF_E_HIP, "k_resident: inter-workgroup hand-off timed out (code " + std::to_string(err) + ")");
+  return PF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -413,6 +512,7 @@ void pf_destroy(pf_handle* h) {
     if (h->lw[k]) (void)hipFree(h->lw[k]);
     if (h->rec[k]) (void)hipFree(h->rec[k]);
   }
+  if (h->rsync) (void)hipFree(h->rsync);
   for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif})
     if (p) (void)hipFree(p);
@@ -592,6 +692,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   if (!d_means || !d_neff || !d_flags || !d_lse) return fail(PF_E_ARG, "device outputs are required");
   if (!h->chol_q_ok) return fail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
   HIPCHK(hipSetDevice(h->device));
+  {
+    bool used = false;
+    h->last_resident = false;
+    pf_status st = run_resident(h, dZ, dU, T, first_update_only, d_means, (h->nx <= 4) ? d_covs : nullptr, d_neff,
+                                d_flags, d_lse, &used);
+    if (st || used) return st;
+  }
   const int R = h->R;
   StepParams p = base_params(h);
   p.o_mean = d_means;
@@ -676,6 +783,8 @@ pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int3
   st = pf_run_device(h, dZ, dU, T, first_update_only, dm, dc, dn, df, dl);
   if (st) return bail(st);
   if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(PF_E_HIP, "pf_run: stream sync failed"));
+  st = check_resident(h);
+  if (st) return bail(st);
   std::vector<int32_t> fl((size_t)T * R);
   if ((means && hipMemcpy(means, dm, (size_t)T * R * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
       (covs && dc && hipMemcpy(covs, dc, (size_t)T * R * nx * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
@@ -905,8 +1014,10 @@ pf_status pf_debug_stamps(unsigned long long* out, int n) {
 pf_status pf_synchronize(pf_handle* h) {
   if (!h) return fail(PF_E_ARG, "null handle");
   HIPCHK(hipStreamSynchronize(h->stream));
-  return PF_OK;
+  return check_resident(h);
 }
+
+int32_t pf_last_run_resident(pf_handle* h) { return (h && h->last_resident) ? 1 : 0; }
 
 pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds) {
   if (!h) return fail(PF_E_ARG, "null handle");

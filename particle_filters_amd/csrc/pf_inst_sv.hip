@@ -16,4 +16,8 @@ void register_sv_models() {
 extern "C" int pf_debug_stamps_sv(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pf::g_pf_stamps), (size_t)n * sizeof(unsigned long long));
 }
+extern "C" int pf_debug_stamps_sv_zero(int n) {
+  static unsigned long long zeros[4096];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pf::g_pf_stamps), zeros, (size_t)(n < 4096 ? n : 4096) * sizeof(unsigned long long));
+}
 #endif

@@ -117,7 +117,7 @@ struct Model {
     observe(x, zp, P);
     Real y[NZ];
     Real quad = Real(0);
-    if (r_diag) {
+    if (NZ == 1 || r_diag) {
 #pragma unroll
       for (int k = 0; k < NZ; ++k) {
         if constexpr (sizeof(Real) == 4)

@@ -9,6 +9,7 @@
 #include <cstdint>
 
 #include "pf_kernels.h"
+#include "pf_resident.h"
 
 namespace pf {
 
@@ -23,6 +24,10 @@ struct Ops {
   hipError_t (*moments)(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,
                         int64_t Npad, int R, double* mean, double* cov, hipStream_t);
   void (*prepare)();  // per-device kernel attributes, called once a device is current
+  // register-resident whole-run kernel (scalar fp32 models only; null otherwise).
+  // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
+  // cannot be co-resident (the caller then runs the launch-per-step path).
+  hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t);
 };
 
 void register_ops(const Ops& o);
@@ -77,6 +82,7 @@ struct Launch {
     o.init = &init;
     o.moments = &moments;
     o.prepare = &prepare;
+    o.resident = nullptr;
     return o;
   }
   static void prepare() {
@@ -95,8 +101,20 @@ void register_l96_models();
 void register_mat_models();
 
 template <int NX, int NZ, int TK, int OK>
+struct ResidentLaunch {
+  static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s) {
+    ResParams q = p;
+    void* args[] = {&q};
+    return hipLaunchCooperativeKernel((const void*)k_resident<float, NX, NZ, TK, OK>, dim3(G, R), dim3(RBS), args,
+                                      0, s);
+  }
+};
+
+template <int NX, int NZ, int TK, int OK>
 inline void register_both() {
-  register_ops(Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32));
+  Ops f32 = Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32);
+  if constexpr (NX == 1) f32.resident = &ResidentLaunch<NX, NZ, TK, OK>::launch;
+  register_ops(f32);
   register_ops(Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64));
 }
 

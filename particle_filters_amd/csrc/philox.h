@@ -63,17 +63,18 @@ struct Normal4 {
 };
 
 // Box-Muller on the two pairs (x, y) and (z, w): r = sqrt(-2 ln u1), angle 2*pi*u2.
+// fp32: the hardware v_sin/v_cos (argument in revolutions, so 2*pi*u2 needs no
+// range reduction), v_log and v_sqrt — a handful of instructions per pair.
 __device__ __forceinline__ Normal4<float> box_muller4(u32x4 r) {
   Normal4<float> n;
-  const float r0 = sqrtf(-2.0f * __logf(u01_f32(r.x)));
-  const float r1 = sqrtf(-2.0f * __logf(u01_f32(r.z)));
-  float s0, c0, s1, c1;
-  sincospif((float)(r.y >> 8) * (2.0f / 16777216.0f), &s0, &c0);
-  sincospif((float)(r.w >> 8) * (2.0f / 16777216.0f), &s1, &c1);
-  n.v[0] = r0 * c0;
-  n.v[1] = r0 * s0;
-  n.v[2] = r1 * c1;
-  n.v[3] = r1 * s1;
+  const float r0 = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_f32(r.x)));
+  const float r1 = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_f32(r.z)));
+  const float a0 = (float)(r.y >> 8) * (1.0f / 16777216.0f);
+  const float a1 = (float)(r.w >> 8) * (1.0f / 16777216.0f);
+  n.v[0] = r0 * __builtin_amdgcn_cosf(a0);
+  n.v[1] = r0 * __builtin_amdgcn_sinf(a0);
+  n.v[2] = r1 * __builtin_amdgcn_cosf(a1);
+  n.v[3] = r1 * __builtin_amdgcn_sinf(a1);
   return n;
 }
 __device__ __forceinline__ Normal4<double> box_muller4_f64(u32x4 r) {

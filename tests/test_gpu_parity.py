@@ -212,9 +212,11 @@ def test_replicate_base_shards_bitwise(golden_sv):
 
 
 @pytest.mark.parametrize("method,reg", [("systematic", False), ("systematic", True), ("multinomial", True)])
-def test_run_equals_step_api(method, reg, golden_sv):
-    """The fused device-resident loop (deferred resample fused into the next step) is
-    bit-identical to predict/update/_resample called one by one."""
+def test_run_equals_step_api(method, reg, golden_sv, monkeypatch):
+    """The launch-per-step device loop (deferred resample fused into the next step) is
+    bit-identical to predict/update/_resample called one by one.  (The register-resident
+    whole-run kernel is compared with this loop in tests/test_gpu_resident.py.)"""
+    monkeypatch.setenv("PF_RESIDENT", "0")
     Y = golden_sv["Y0"]
     Z = np.log(Y[1:120] ** 2)[:, None]
 
