@@ -48,25 +48,42 @@ constexpr int RMAXG = 256;         // workgroups per replicate (<= CUs: all co-r
 constexpr int RCW = RMAXG / 64;    // waves that hold one record each per lane when verifying
 constexpr int RRING = 8;           // record ring slots (>= 2*LAG + 2)
 constexpr int RF = 7;              // record granules: M, S0, S00, S1, S2, A1, A2
-constexpr int RLAG = 2;            // verification lag (steps)
+#ifndef PF_RLAG
+#define PF_RLAG 2
+#endif
+constexpr int RLAG = PF_RLAG;      // verification lag (steps)
 constexpr unsigned RSPIN_LIMIT = 1u << 24;
+constexpr int RSTAGE = 8192;       // rollback scatter staging chunk (floats of LDS)
 
 // Diagnostic phase accounting (PF_STAMPS builds only): workgroup 0, thread 0
 // accumulates s_memrealtime ticks (100 MHz) per phase into g_pf_stamps[0..15].
 #ifdef PF_STAMPS
-#define PF_RMARK(k)                                                      \
-  do {                                                                   \
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {        \
-      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
-      g_pf_stamps[(k)] += now_ - rstamp_last;                            \
-      rstamp_last = now_;                                                \
-    }                                                                    \
+// accumulated in registers (thread 0 of workgroup 0), written once at the end
+#define PF_RMARK(k)                                                     \
+  do {                                                                  \
+    if (stamp_me) {                                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); \
+      racc[(k)] += now_ - rstamp_last;                                  \
+      rstamp_last = now_;                                               \
+    }                                                                   \
   } while (0)
-#define PF_RCOUNT(k)                                                                    \
-  do {                                                                                  \
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_pf_stamps[(k)] += 1; \
+#define PF_RCOUNT(k)            \
+  do {                          \
+    if (stamp_me) racc[(k)] += 1; \
+  } while (0)
+// rare-path phases (rollback): global accumulators, thread 0 of workgroup 0
+#define PF_GMARK(k)                                                                   \
+  do {                                                                                \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();               \
+      g_pf_stamps[(k)] += now_ - gstamp_last;                                         \
+      gstamp_last = now_;                                                             \
+    }                                                                                 \
   } while (0)
 #else
+#define PF_GMARK(k) \
+  do {              \
+  } while (0)
 #define PF_RMARK(k) \
   do {              \
   } while (0)
@@ -74,6 +91,9 @@ constexpr unsigned RSPIN_LIMIT = 1u << 24;
   do {               \
   } while (0)
 #endif
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr int PF_AUX_SC1 = 16;  // buffer instruction cache-policy bits: sc1 (write-through / L1 bypass)
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -229,22 +249,47 @@ __device__ __forceinline__ double wave_sum_ud(double v) {
   return lane63_d(v);
 }
 
-// Rollback hand-off + systematic resampling of one step (pf.py:146-171, 188-218)
-// for the tile of workgroup b.  The step's pre-resample state is this thread's
-// snapshot slot (sx_slot / sl_slot); the resampled (and jittered) particles are
-// written back into sx_slot.  Out of line: it runs on ~5% of steps and its fp64
-// position arithmetic must not occupy registers in the step loop.
-// Returns false if the hand-off timed out.
+// Number of systematic positions below x: #{ i in [0, N) : (U + i) / N < x },
+// evaluated with the very comparison the reference makes (pf.py:146-171: pos =
+// (U + arange(N)) / N in fp64, ancestor = first j with pos < cdf[j]).
+__device__ __forceinline__ int64_t count_below(double x, double U, int64_t N) {
+  // exactly, (U + i) / N < x  <=>  i < y = x N - U; the fp64 division can only
+  // disagree when (U + i) / N lies within an ulp of x, i.e. when y is within
+  // ~1e-10 of an integer: only then are the candidate positions evaluated the
+  // reference's way.
+  const double Nd = (double)N;
+  const double y = fma(x, Nd, -U);
+  const double c0 = ceil(y);
+  if (c0 - y > 1e-7 && y - (c0 - 1.0) > 1e-7) return (int64_t)fmin(fmax(c0, 0.0), Nd);
+  int64_t c = (int64_t)fmin(fmax(c0, 0.0), Nd);
+  while (c > 0 && (U + (double)(c - 1)) / Nd >= x) --c;
+  while (c < N && (U + (double)c) / Nd < x) ++c;
+  return c;
+}
+
+// Rollback + systematic resampling of one step (pf.py:146-171, 188-218), source-
+// driven: workgroup b owns input tile b (its snapshot in LDS), builds that tile's
+// fp64 CDF segment, and writes each particle into its offspring slots
+// [C(cdf_{j-1}), C(cdf_j)) of the gathered array — no remote tile reads, work per
+// workgroup proportional to its tile's offspring.  Two grid hand-offs: the exact
+// tile sums (for the global prefix), then the gathered array.  The resampled
+// (and jittered) particles of this workgroup's output slots land in sx_slot.
+// Out of line: it runs on ~5% of steps and its fp64 position arithmetic must not
+// occupy registers in the step loop.  Returns false if a hand-off timed out.
 template <typename Real, int NX, int NZ, int TK, int OK>
-__device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long* sflag, double* tsum,
-                                       unsigned* err, unsigned* err_sh, float4* sx_slot, const float4* sl_slot,
-                                       double* red, double* Pl, double* Ck, float* Mk, double* cdf, int G, int b,
-                                       int64_t N, unsigned nres, float m_g, float s0_g, double Mx, uint64_t seed,
-                                       uint32_t rep, uint32_t ep_res, int regularize, const Real* P) {
+__device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, double* tsum, unsigned* err,
+                                       unsigned* err_sh, float4* sx_slot, const float4* sl_slot, double* red,
+                                       double* Pl, double* Ck, double* offs, float* stage, int G, int b, int64_t N,
+                                       unsigned nres,
+                                       float m_g, float s0_g, double Mx, uint64_t seed, uint32_t rep,
+                                       uint32_t ep_res, int regularize, const Real* P) {
   using Mo = Model<Real, NX, NZ, TK, OK>;
   const int t = threadIdx.x;
   const int64_t o0 = (int64_t)b * RTILE;
   const int64_t i0 = o0 + RPPT * (int64_t)t;
+#ifdef PF_STAMPS
+  unsigned long long gstamp_last = __builtin_amdgcn_s_memrealtime();
+#endif
   float xv[RPPT], lv[RPPT];
 #pragma unroll
   for (int q = 0; q < RPV; ++q) {
@@ -252,8 +297,7 @@ __device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long*
     xv[4 * q] = xs.x; xv[4 * q + 1] = xs.y; xv[4 * q + 2] = xs.z; xv[4 * q + 3] = xs.w;
     lv[4 * q] = ls.x; lv[4 * q + 1] = ls.y; lv[4 * q + 2] = ls.z; lv[4 * q + 3] = ls.w;
   }
-  // this tile's exact weight sum, by the very procedure every reader uses to
-  // build its CDF below (so the tile's last CDF value meets the next prefix)
+  // ---- this tile's weights relative to its max, exclusive prefix, exact sum --
   float mown = -INFINITY;
 #pragma unroll
   for (int e = 0; e < RPPT; ++e) mown = fmaxf(mown, lv[e]);  // slots past N hold -inf
@@ -265,27 +309,28 @@ __device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long*
 #pragma unroll
     for (int j = 0; j < RNW; ++j) mown = fmaxf(mown, (float)red[64 + j]);
   }
-  double own = 0.0;
+  double wv[RPPT];
+  double part = 0.0;
 #pragma unroll
-  for (int e = 0; e < RPPT; ++e) own += (lv[e] > -INFINITY) ? (double)exp_r<float>(lv[e] - mown) : 0.0;
+  for (int e = 0; e < RPPT; ++e) {
+    wv[e] = (lv[e] > -INFINITY) ? (double)exp_r<float>(lv[e] - mown) : 0.0;
+    part += wv[e];
+  }
   double Town;
-  (void)block_excl_scan<RBS>(own, red, &Town);
-  // hand the snapshot to every workgroup: sc1 stores, drain, barrier, one flag
-#pragma unroll
-  for (int e = 0; e < RPPT; ++e)
-    if (i0 + e < N) {
-      st_sc1_f(xg + i0 + e, xv[e]);
-      st_sc1_f(lg + i0 + e, lv[e]);
-    }
-  if (t == 0) __hip_atomic_store((gu64*)(tsum + b), (unsigned long long)__double_as_longlong(Town), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+  const double off = block_excl_scan<RBS>(part, red, &Town);
+  offs[t] = off;
+  PF_GMARK(6);
+  // ---- hand-off 1: the exact tile sums ----------------------------------------
+  if (t == 0)
+    __hip_atomic_store((gu64*)(tsum + b), (unsigned long long)__double_as_longlong(Town), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) st_sc1(sflag + b, (unsigned long long)nres);
-  // wait for every snapshot
+  const unsigned long long f1 = 2ull * nres - 1, f2 = 2ull * nres;
+  if (t == 0) st_sc1(sflag + b, f1);
   for (unsigned spins = 0;; ++spins) {
     int good = 1;
-    if (t < G) good = ld_sc1(sflag + t) == (unsigned long long)nres;
+    if (t < G) good = ld_sc1(sflag + t) >= f1;
     if (__syncthreads_and(good)) break;
     if (spins >= RSPIN_LIMIT) {
       if (t == 0) {
@@ -296,7 +341,8 @@ __device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long*
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  // global tile prefix in fp64 from the exact tile sums (fixed order)
+  PF_GMARK(7);
+  // ---- global tile prefix in fp64 (fixed order: identical in every workgroup) -
   double fg = 0.0, wg = 0.0;
   if (t < G && s0_g > 0.0f) {
     fg = exp((double)m_g - Mx);
@@ -307,50 +353,88 @@ __device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long*
   if (t < G) {
     Pl[t] = run / Stot;
     Ck[t] = fg / Stot;
-    Mk[t] = m_g;
   }
-  if (t == 0) Pl[G] = 1.0;
+  if (t == 0) Pl[G] = 1.0;  // the reference's cdf[-1] = 1.0
   __syncthreads();
-  // systematic positions (U + i) / N of this tile's slots, ancestors by tile CDF
+  PF_GMARK(8);
+  // ---- offspring ranges of this tile's particles ------------------------------
+  // particle j of the tile takes output slots [C(cdf_{j-1}), C(cdf_j)); the whole
+  // tile takes the contiguous range [C(Pl[b]), C(Pl[b+1])), staged through LDS
+  // in chunks and written with coalesced 16-byte sc1 stores.
   const double U = uniform53(seed, 0, rep, ep_res);
-  const int64_t last = min(o0 + (int64_t)RTILE, N) - 1;
-  const int k_lo = prefix_tile(Pl, G, (U + (double)o0) / (double)N);
-  const int k_hi = prefix_tile(Pl, G, (U + (double)last) / (double)N);
-  int anc[RPPT];
-#pragma unroll
-  for (int e = 0; e < RPPT; ++e) anc[e] = -1;
-  for (int k = k_lo; k <= k_hi; ++k) {
-    if (!(Pl[k + 1] > Pl[k])) continue;  // no mass: no position lands here
-    const int64_t sk = (int64_t)k * RTILE;
-    const int len = (int)min((int64_t)RTILE, N - sk);
-    const float mk = Mk[k];
-    float lt[RPPT];
-    double part = 0.0;
+  const double base = Pl[b], hi = Pl[b + 1], c = Ck[b];
+  const int64_t tile_last = min(o0 + (int64_t)RTILE, N) - 1;
+  int64_t cb[RPPT + 1];  // cb[e] .. cb[e+1]: slots of particle i0 + e (empty past the tile)
+  {
+    const double xb = (i0 + RPPT - 1 >= tile_last) ? hi : base + c * offs[t + 1];
+    cb[0] = (i0 <= tile_last) ? count_below(base + c * off, U, N) : 0;
+    double cum = off;
 #pragma unroll
     for (int e = 0; e < RPPT; ++e) {
-      const int j = RPPT * t + e;
-      lt[e] = j < len ? ld_sc1_f(lg + sk + j) : -INFINITY;
-      part += (lt[e] > -INFINITY) ? (double)exp_r<float>(lt[e] - mk) : 0.0;
+      const int64_t j = i0 + e;
+      if (j > tile_last) {
+        cb[e + 1] = cb[e];
+        continue;
+      }
+      cum += wv[e];
+      const double xe = (e == RPPT - 1 || j == tile_last) ? xb : fmin(base + c * cum, xb);
+      cb[e + 1] = max(count_below(xe, U, N), cb[e]);
     }
-    double tot;
-    double off = block_excl_scan<RBS>(part, red, &tot);
-    const double c = Ck[k], base = Pl[k];
+  }
+  const int64_t R0 = count_below(base, U, N), R1 = count_below(hi, U, N);
+  for (int64_t cs = R0; cs < R1; cs += RSTAGE) {
+    const int64_t ce = min(cs + (int64_t)RSTAGE, R1);
 #pragma unroll
     for (int e = 0; e < RPPT; ++e) {
-      const int j = RPPT * t + e;
-      off += (lt[e] > -INFINITY) ? (double)exp_r<float>(lt[e] - mk) : 0.0;
-      if (j < len) cdf[j] = base + c * off;
+      const int64_t a0 = max(cb[e], cs), a1 = min(cb[e + 1], ce);
+      for (int64_t i = a0; i < a1; ++i) stage[i - cs] = xv[e];
     }
     __syncthreads();
-#pragma unroll
-    for (int e = 0; e < RPPT; ++e) {
-      const int64_t i = i0 + e;
-      if (i < N && anc[e] < 0) {
-        const double pos = (U + (double)i) / (double)N;
-        if (prefix_tile(Pl, G, pos) == k) anc[e] = (int)(sk + lds_upper(cdf, len, pos));
+    // coalesced write of stage[0, ce - cs) to xn[cs, ce): unaligned head/tail scalar
+    const int64_t body0 = (cs + 3) & ~(int64_t)3, body1 = ce & ~(int64_t)3;
+    if (body0 >= body1) {
+      for (int64_t i = cs + t; i < ce; i += RBS) st_sc1_f(xn + i, stage[i - cs]);
+    } else {
+      if (t < body0 - cs) st_sc1_f(xn + cs + t, stage[t]);
+      if (t < ce - body1) st_sc1_f(xn + body1 + t, stage[body1 - cs + t]);
+      const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(xn, 0, (int)(N * 4), 0x00020000);
+      for (int64_t i = body0 + 4 * (int64_t)t; i < body1; i += 4 * RBS) {
+        const int64_t k = i - cs;
+        const v4f v = {stage[k], stage[k + 1], stage[k + 2], stage[k + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rw, (int)(i * 4), 0, PF_AUX_SC1);
       }
     }
-    __syncthreads();  // the CDF is rebuilt for the next tile
+    __syncthreads();  // stage is refilled by the next chunk
+  }
+  PF_GMARK(9);
+  // ---- hand-off 2: the gathered array -----------------------------------------
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) st_sc1(sflag + b, f2);
+  for (unsigned spins = 0;; ++spins) {
+    int good = 1;
+    if (t < G) good = ld_sc1(sflag + t) >= f2;
+    if (__syncthreads_and(good)) break;
+    if (spins >= RSPIN_LIMIT) {
+      if (t == 0) {
+        *err_sh = 1;
+        atomicOr(err, 2u);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  PF_GMARK(10);
+  // ---- this workgroup's output slots: gathered ancestors + jitter -------------
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(xn, 0, (int)(N * 4), 0x00020000);
+  float xg8[RPPT];
+#pragma unroll
+  for (int q = 0; q < RPV; ++q) {
+    const v4f v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((i0 + 4 * q) * 4), 0, PF_AUX_SC1);
+    xg8[4 * q] = v.x;
+    xg8[4 * q + 1] = v.y;
+    xg8[4 * q + 2] = v.z;
+    xg8[4 * q + 3] = v.w;
   }
   Real nj[RPPT];
 #pragma unroll
@@ -363,22 +447,19 @@ __device__ __noinline__ bool rb_gather(float* xg, float* lg, unsigned long long*
       for (int e = 0; e < 4; ++e) nj[4 * q + e] = nq.v[e];
     }
   }
-  float xn[RPPT];
+  float xo[RPPT];
 #pragma unroll
   for (int e = 0; e < RPPT; ++e) {
-    xn[e] = 0.0f;
-    if (i0 + e < N) {
-      const int a = anc[e] < 0 ? (int)(N - 1) : anc[e];
-      Real xe[1] = {ld_sc1_f(xg + a)};
-      if (regularize) {
-        Real n[1] = {nj[e]};
-        Mo::add_lower(xe, n, P, Mo::L::LJ);
-      }
-      xn[e] = xe[0];
+    Real xe[1] = {xg8[e]};
+    if (regularize) {
+      Real n[1] = {nj[e]};
+      Mo::add_lower(xe, n, P, Mo::L::LJ);
     }
+    xo[e] = (i0 + e < N) ? xe[0] : 0.0f;
   }
 #pragma unroll
-  for (int q = 0; q < RPV; ++q) sx_slot[q * RBS + t] = make_float4(xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+  for (int q = 0; q < RPV; ++q) sx_slot[q * RBS + t] = make_float4(xo[4 * q], xo[4 * q + 1], xo[4 * q + 2], xo[4 * q + 3]);
+  PF_GMARK(11);
   return true;
 }
 
@@ -391,15 +472,17 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   constexpr int LAG = RLAG;
   constexpr int NSNAP = LAG + 1;
   __shared__ __attribute__((aligned(16))) double red[LDS_RED];
-  __shared__ double mslot[RNW][8];  // per-wave partials of this workgroup's step record
-  __shared__ double cslot[RCW][8];  // per-wave partials of a verified step's summary
+  // per-wave partials, double-buffered by iteration parity: with ONE barrier per
+  // iteration a wave is at most one iteration ahead of any other
+  __shared__ double mslot[2][RNW][8];  // this workgroup's step record
+  __shared__ double cslot[2][RCW][8];  // the verified step's summary (+ tags-complete flag)
   __shared__ int okw[RNW];
-  __shared__ double sF[NSNAP];  // frame of each snapshot slot
+  __shared__ double sF[NSNAP];     // frame of each snapshot slot
   __shared__ long long sT[NSNAP];  // filter step of each snapshot slot
   __shared__ double Pl[RMAXG + 1];
   __shared__ double Ck[RMAXG];
-  __shared__ float Mk[RMAXG];
-  __shared__ __attribute__((aligned(16))) double cdf[RTILE];
+  __shared__ double offs[RBS];
+  __shared__ float stage[RSTAGE];
   __shared__ unsigned err_sh;
   // snapshot ring, thread-private slots: state after each of the last LAG+1 steps
   __shared__ float4 snx[NSNAP][RPV * RBS];
@@ -420,10 +503,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const float lunif = (float)(-pf_dlog((double)N));
   const unsigned long long* gbase = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
-  unsigned long long rstamp_last = 0;
-  (void)rstamp_last;
 #ifdef PF_STAMPS
-  if (b == 0 && r == 0 && t == 0) rstamp_last = __builtin_amdgcn_s_memrealtime();
+  const bool stamp_me = b == 0 && r == 0 && t == 0;
+  unsigned long long racc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) racc[k] = 0;
+  unsigned long long rstamp_last = __builtin_amdgcn_s_memrealtime();
 #endif
 
   // ---- entry state (k_step layout) and its normaliser ------------------------
@@ -441,12 +526,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     }
   }
 
-
   const int fo = p.first_update_only ? 1 : 0;
   int64_t tstep = 0;       // next filter step to compute
   unsigned s_next = 0;     // next sequence number (executed steps, incl. discarded ones)
   unsigned vnext = 0;      // next sequence number to verify
   unsigned nres = 0;       // hand-offs so far (flag tags)
+  unsigned it = 0;         // iteration parity (LDS double buffers)
   double F = 0.0;          // frame of the live log-weights
   double Tprev = 0.0;      // absolute log mass of the last verified step
   bool prev_res = false;   // last verified step resampled: next record carries its aux sums
@@ -454,21 +539,43 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   double aux1 = 0.0, aux2 = 0.0;
   bool last_uniform = false;
   bool alive = true;
+  unsigned long long pg[RF];  // granules of the step being verified (waves 0..RCW-1: one record per lane)
+#pragma unroll
+  for (int f = 0; f < RF; ++f) pg[f] = 0;
 
   while (alive) {
     const bool computing = tstep < p.T;
     const unsigned s_after = s_next + (computing ? 1u : 0u);
+#if defined(PF_ABLATE) && PF_ABLATE == 1
+    const bool verify = false;  // ablation: no verification at all (timing floor of the step)
+    if (!computing) break;
+#else
     const bool verify =
         vnext < s_after && (s_after - vnext > (unsigned)LAG || tstep + (computing ? 1 : 0) >= p.T);
+#endif
     if (!computing && !verify) break;
-
-    // ---------------- prefetch the records to verify (overlaps the step) -----
-    unsigned long long pg[RF];
-    const unsigned vtag = vnext + 1;
-    const unsigned long long* vbase = gbase + (size_t)(vnext % RRING) * RF * RMAXG + t;
-    if (verify && t < G) {
+    const int cur = (int)(it & 1u);
+    ++it;
+    const unsigned v = vnext;
+    const unsigned vtag = v + 1;
+    const unsigned long long* vbase = gbase + (size_t)(v % RRING) * RF * RMAXG + t;
+    const int idx = (int)(v % NSNAP);  // snapshot slot of step v
+    double Fv = 0.0;
+    int64_t tv = 0;
+    if (verify) {
+      // granule loads for v (their latency overlaps the step below); slot info
+      // read before this iteration's barrier (written iterations ago)
+      if (t < G) {
 #pragma unroll
-      for (int f = 0; f < RF; ++f) pg[f] = ld_sc1(vbase + f * RMAXG);
+        for (int f = 0; f < RF; ++f) pg[f] = ld_sc1(vbase + f * RMAXG);
+      }
+      if (computing && v == s_next) {  // verifying the step computed right now (T=1 / drain)
+        Fv = F;
+        tv = tstep;
+      } else {
+        Fv = uni(sF[idx]);
+        tv = uni_i64(sT[idx]);
+      }
     }
     PF_RMARK(0);
 
@@ -509,7 +616,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         x[e] = xe[0];
         l[e] = l[e] + Mo::loglik(xe, z, P, p.r_diag != 0);
       }
-      // this thread's max-first partial sums (invalid slots hold l = -inf)
+      // this thread's max-first partial sums
       float m = l[0];
 #pragma unroll
       for (int e = 1; e < RPPT; ++e) m = fmaxf(m, l[e]);
@@ -536,13 +643,13 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         a2 = wave_sum_ud(aux2);
       }
       if (lane == 0) {
-        mslot[w][0] = Mw;
-        mslot[w][1] = w0;
-        mslot[w][2] = w00;
-        mslot[w][3] = w1;
-        mslot[w][4] = w2;
-        mslot[w][5] = a1;
-        mslot[w][6] = a2;
+        mslot[cur][w][0] = Mw;
+        mslot[cur][w][1] = w0;
+        mslot[cur][w][2] = w00;
+        mslot[cur][w][3] = w1;
+        mslot[cur][w][4] = w2;
+        mslot[cur][w][5] = a1;
+        mslot[cur][w][6] = a2;
       }
       {  // snapshot of this step in slot s_next % NSNAP
         const int slot = (int)(s_next % NSNAP);
@@ -556,216 +663,243 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           sT[slot] = tstep;
         }
       }
-      __syncthreads();
-      if (w == 0) {  // combine the 16 wave partials (row 0 of wave 0) and publish
-        const bool in = lane < RNW;
-        const float mj = in ? (float)mslot[lane][0] : -INFINITY;
-        const float Mt = row_max_f(mj);
-        const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
-        const float t0 = row_sum_f(in ? (float)mslot[lane][1] * fj : 0.0f);
-        const float t00 = row_sum_f(in ? (float)mslot[lane][2] * fj * fj : 0.0f);
-        const float t1 = row_sum_f(in ? (float)mslot[lane][3] * fj : 0.0f);
-        const float t2 = row_sum_f(in ? (float)mslot[lane][4] * fj : 0.0f);
-        const double ta1 = row_sum_d(in ? mslot[lane][5] : 0.0);
-        const double ta2 = row_sum_d(in ? mslot[lane][6] : 0.0);
-        if (lane == 0) {  // 7 granules, each one sc1 store (the data is its own flag)
-          const unsigned tag = s_next + 1;
-          unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + 0 * RMAXG, granule(tag, Mt));
-          st_sc1(g + 1 * RMAXG, granule(tag, t0));
-          st_sc1(g + 2 * RMAXG, granule(tag, t00));
-          st_sc1(g + 3 * RMAXG, granule(tag, t1));
-          st_sc1(g + 4 * RMAXG, granule(tag, t2));
-          st_sc1(g + 5 * RMAXG, granule(tag, (float)ta1));
-          st_sc1(g + 6 * RMAXG, granule(tag, (float)ta2));
-        }
-      }
-      PF_RMARK(2);
-      PF_RCOUNT(14);
       have_aux = false;
-      ++s_next;
-      ++tstep;
     }
 
-    // ---------------- verify the oldest unverified step ----------------------
-    if (verify) {
-      const unsigned v = vnext;
-      const int idx = (int)(v % NSNAP);  // snapshot slot of step v
-      const double Fv = uni(sF[idx]);  // written before the step's barrier
-      const int64_t tv = uni_i64(sT[idx]);
-      // all tags in? (the prefetched loads usually are)
+    // ---------------- wave-level summary of the step being verified ----------
+    const bool in = t < G;
+    float m_g = -INFINITY, s0_g = 0.0f;
+    if (verify && w < RCW) {
       int good = 1;
-      if (t < G) {
+      if (in) {
 #pragma unroll
         for (int f = 0; f < RF; ++f) good &= (unsigned)(pg[f] >> 32) == vtag;
       }
-      for (unsigned spins = 0;; ++spins) {
-        const int wg = __all(good);
-        if (lane == 0) okw[w] = wg;
-        __syncthreads();
-        int all = 1;
-#pragma unroll
-        for (int j = 0; j < RCW; ++j) all &= okw[j];
-        all = __builtin_amdgcn_readfirstlane(all);
-        if (all) break;
-        __syncthreads();  // okw is rewritten below
-        PF_RCOUNT(15);
-        if (spins >= RSPIN_LIMIT) {
-          if (t == 0) {
-            err_sh = 1;
-            atomicOr(p.err, 1u);
-          }
-          alive = false;
-          break;
+      m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
+      s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
+      const float mg = (s0_g > 0.0f) ? m_g : -INFINITY;
+      const float Mw = wave_max_u(mg);
+      const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
+      const double d0 = wave_sum_ud((double)s0_g * f);
+      const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
+      const double d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
+      const double d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
+      const double d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
+      const double d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+      const int wgood = __all(good);
+      if (lane == 0) {
+        cslot[cur][w][0] = Mw;
+        cslot[cur][w][1] = d0;
+        cslot[cur][w][2] = d1;
+        cslot[cur][w][3] = d2;
+        cslot[cur][w][4] = d3;
+        cslot[cur][w][5] = d4;
+        cslot[cur][w][6] = d5;
+        cslot[cur][w][7] = wgood ? 1.0 : 0.0;
+      }
+    }
+    __syncthreads();  // the iteration's one barrier
+    PF_RMARK(2);
+
+    // ---------------- publish this workgroup's record ------------------------
+    if (computing) {
+      if (w == 0) {  // combine the wave partials (row 0 of wave 0); lanes 0..6 publish
+        const int j = lane & (RNW - 1);
+        const bool inr = lane < RNW;
+        const double* ms = mslot[cur][j];
+        const double v0 = ms[0], v1 = ms[1], v2 = ms[2], v3 = ms[3], v4 = ms[4], v5 = ms[5], v6 = ms[6];
+        const float mj = inr ? (float)v0 : -INFINITY;
+        const float Mt = row_max_f(mj);
+        const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
+        const float t0 = row_sum_f(inr ? (float)v1 * fj : 0.0f);
+        const float t00 = row_sum_f(inr ? (float)v2 * fj * fj : 0.0f);
+        const float t1 = row_sum_f(inr ? (float)v3 * fj : 0.0f);
+        const float t2 = row_sum_f(inr ? (float)v4 * fj : 0.0f);
+        const double ta1 = row_sum_d(inr ? v5 : 0.0);
+        const double ta2 = row_sum_d(inr ? v6 : 0.0);
+        if (lane < RF) {  // 7 granules, one sc1 store each (the data is its own flag)
+          const float val = lane == 0 ? Mt : lane == 1 ? t0 : lane == 2 ? t00 : lane == 3 ? t1 : lane == 4 ? t2
+                          : lane == 5 ? (float)ta1 : (float)ta2;
+          unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+          st_sc1(g + lane * RMAXG, granule(s_next + 1, val));
         }
-        __builtin_amdgcn_s_sleep(2);
-        good = 1;
-        if (t < G) {
+      }
+      PF_RCOUNT(14);
+      ++s_next;
+      ++tstep;
+    }
+    PF_RMARK(3);
+    if (!verify) continue;
+
+    // ---------------- verify step v -------------------------------------------
+    int all = 1;
+#pragma unroll
+    for (int j = 0; j < RCW; ++j) all &= cslot[cur][j][7] != 0.0;
+    all = __builtin_amdgcn_readfirstlane(all);
+    PF_RMARK(4);
+    for (unsigned spins = 0; !all; ++spins) {  // slow path: not every record was in yet
+      PF_RCOUNT(15);
+      __syncthreads();  // every wave has read cslot[cur]
+      if (spins >= RSPIN_LIMIT) {
+        if (t == 0) {
+          err_sh = 1;
+          atomicOr(p.err, 1u);
+        }
+        alive = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if (w < RCW) {
+        int good = 1;
+        if (in) {
 #pragma unroll
           for (int f = 0; f < RF; ++f) {
             pg[f] = ld_sc1(vbase + f * RMAXG);
             good &= (unsigned)(pg[f] >> 32) == vtag;
           }
         }
-      }
-      if (!alive) break;
-      PF_RMARK(3);
-      // summary of the step: waves 0..RCW-1 hold one record per lane
-      const bool in = t < G;
-      const float m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
-      const float s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
-      float fl_g = 0.0f;  // e^(m_g - wave max)
-      if (w < RCW) {
+        m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
+        s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
         const float mg = (s0_g > 0.0f) ? m_g : -INFINITY;
         const float Mw = wave_max_u(mg);
-        fl_g = (mg > -INFINITY) ? __expf(mg - Mw) : 0.0f;
-        const double f = (double)fl_g;
+        const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
         const double d0 = wave_sum_ud((double)s0_g * f);
         const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
         const double d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
         const double d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
         const double d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
         const double d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+        const int wgood = __all(good);
         if (lane == 0) {
-          cslot[w][0] = Mw;
-          cslot[w][1] = d0;
-          cslot[w][2] = d1;
-          cslot[w][3] = d2;
-          cslot[w][4] = d3;
-          cslot[w][5] = d4;
-          cslot[w][6] = d5;
+          cslot[cur][w][0] = Mw;
+          cslot[cur][w][1] = d0;
+          cslot[cur][w][2] = d1;
+          cslot[cur][w][3] = d2;
+          cslot[cur][w][4] = d3;
+          cslot[cur][w][5] = d4;
+          cslot[cur][w][6] = d5;
+          cslot[cur][w][7] = wgood ? 1.0 : 0.0;
         }
       }
       __syncthreads();
-      double Mx = -INFINITY;
+      all = 1;
 #pragma unroll
-      for (int j = 0; j < RCW; ++j) Mx = fmax(Mx, cslot[j][0]);
-      Mx = uni(Mx);
-      double W = 0.0, W2 = 0.0, S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
+      for (int j = 0; j < RCW; ++j) all &= cslot[cur][j][7] != 0.0;
+      all = __builtin_amdgcn_readfirstlane(all);
+    }
+    if (!alive) break;
+    PF_RMARK(12);  // slow polls
+    double Mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < RCW; ++j) {
-        const double mj = cslot[j][0];
-        const double Fj = (mj > -INFINITY) ? (double)__expf((float)(mj - Mx)) : 0.0;
-        W += cslot[j][1] * Fj;
-        W2 += cslot[j][2] * Fj * Fj;
-        S1 += cslot[j][3] * Fj;
-        S2 += cslot[j][4] * Fj;
-        A1 += cslot[j][5];
-        A2 += cslot[j][6];
-      }
-      W = uni(W);
-      W2 = uni(W2);
-      S1 = uni(S1);
-      S2 = uni(S2);
-      A1 = uni(A1);
-      A2 = uni(A2);
-      PF_RMARK(4);
-      const double lse_rel = Mx + log_pos(W);
-      const double neff = (W * W) / W2;
-      const bool dec = neff < p.thresh * (double)N;
-      const double Tv = lse_rel + Fv;
-      if (b == 0 && t == 0) {
-        const int64_t o = tv * R + r;
-        p.o_neff[o] = neff;
-        p.o_lse[o] = Tv - Tprev;
-        p.o_flag[o] = dec ? 1 : 0;
-        const double mean = S1 / W;
-        p.o_mean[o] = mean;
-        if (p.o_cov) p.o_cov[o] = S2 / W - mean * mean;
-        if (prev_res) {  // post-resample moments of step tv - 1 (uniform weights)
-          const int64_t o2 = (tv - 1) * R + r;
-          const double mp = A1 / (double)N;
-          p.o_mean[o2] = mp;
-          if (p.o_cov) p.o_cov[o2] = A2 / (double)N - mp * mp;
-        }
-      }
-      prev_res = false;
-      if (!dec) {
-        Tprev = Tv;
-        const float delta = (float)(Tv - F);
+    for (int j = 0; j < RCW; ++j) Mx = fmax(Mx, cslot[cur][j][0]);
+    Mx = uni(Mx);
+    double W = 0.0, W2 = 0.0, S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
 #pragma unroll
-        for (int e = 0; e < RPPT; ++e) l[e] = l[e] - delta;  // -inf stays -inf
-        F += (double)delta;
-        vnext = v + 1;
-        last_uniform = false;
-      } else {
-        // ---- rollback to step tv and resample it (out of line: rare) ----------
-        PF_RCOUNT(13);
-        ++nres;
-        const uint32_t ep_res = p.ep0 + (uint32_t)(2 * tv + 1) - fo;
-        if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.lg + rN, p.sflag + (size_t)r * RMAXG,
-                                              p.tsum + (size_t)r * RMAXG, p.err, &err_sh, snx[idx], snl[idx], red,
-                                              Pl, Ck, Mk, cdf, G, b, N, nres, m_g, s0_g, Mx, p.seed, rep, ep_res,
-                                              p.regularize, (const Real*)p.P)) {
-          alive = false;
-          break;
-        }
-#pragma unroll
-        for (int q = 0; q < RPV; ++q) {
-          const float4 xs = snx[idx][q * RBS + t];
-          x[4 * q] = xs.x;
-          x[4 * q + 1] = xs.y;
-          x[4 * q + 2] = xs.z;
-          x[4 * q + 3] = xs.w;
-        }
-        aux1 = 0.0;
-        aux2 = 0.0;
-#pragma unroll
-        for (int e = 0; e < RPPT; ++e) {
-          if (i0 + e < N) {
-            l[e] = lunif;
-            aux1 += (double)x[e];
-            aux2 += (double)x[e] * (double)x[e];
-          } else {
-            x[e] = 0.0f;
-            l[e] = -INFINITY;
-          }
-        }
-        PF_RMARK(5);
-        have_aux = true;
-        prev_res = true;
-        last_uniform = true;
-        F = 0.0;
-        Tprev = 0.0;
-        tstep = tv + 1;
-        vnext = s_next;  // the speculative steps after tv are discarded
+    for (int j = 0; j < RCW; ++j) {
+      const double mj = cslot[cur][j][0];
+      const double Fj = (mj > -INFINITY) ? (double)__expf((float)(mj - Mx)) : 0.0;
+      W += cslot[cur][j][1] * Fj;
+      W2 += cslot[cur][j][2] * Fj * Fj;
+      S1 += cslot[cur][j][3] * Fj;
+      S2 += cslot[cur][j][4] * Fj;
+      A1 += cslot[cur][j][5];
+      A2 += cslot[cur][j][6];
+    }
+    W = uni(W);
+    W2 = uni(W2);
+    S1 = uni(S1);
+    S2 = uni(S2);
+    A1 = uni(A1);
+    A2 = uni(A2);
+    PF_RMARK(4);
+    const double lse_rel = Mx + log_pos(W);
+#if defined(PF_ABLATE) && PF_ABLATE == 2
+    const bool dec = false;  // ablation: never resample (cost of verification without rollbacks)
+#else
+    const bool dec = W * W < p.thresh * (double)N * W2;  // Neff = W^2 / W2 < thresh * N
+#endif
+    const double Tv = lse_rel + Fv;
+    if (b == G - 1 && t == 0) {  // outputs: the last workgroup (the partial tile, least work)
+      const int64_t o = tv * R + r;
+      p.o_neff[o] = (W * W) / W2;
+      p.o_lse[o] = Tv - Tprev;
+      p.o_flag[o] = dec ? 1 : 0;
+      const double mean = S1 / W;
+      p.o_mean[o] = mean;
+      if (p.o_cov) p.o_cov[o] = S2 / W - mean * mean;
+      if (prev_res) {  // post-resample moments of step tv - 1 (uniform weights)
+        const int64_t o2 = (tv - 1) * R + r;
+        const double mp = A1 / (double)N;
+        p.o_mean[o2] = mp;
+        if (p.o_cov) p.o_cov[o2] = A2 / (double)N - mp * mp;
       }
     }
+    prev_res = false;
+    if (!dec) {
+      Tprev = Tv;
+      const float delta = (float)(Tv - F);
+#pragma unroll
+      for (int e = 0; e < RPPT; ++e) l[e] = l[e] - delta;  // -inf stays -inf
+      F += (double)delta;
+      vnext = v + 1;
+      last_uniform = false;
+      continue;
+    }
+    // ---- rollback to step tv and resample it (out of line: rare) --------------
+    PF_RCOUNT(13);
+    ++nres;
+    const uint32_t ep_res = p.ep0 + (uint32_t)(2 * tv + 1) - fo;
+    if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.sflag + (size_t)r * RMAXG, p.tsum + (size_t)r * RMAXG,
+                                          p.err, &err_sh, snx[idx], snl[idx], red, Pl, Ck, offs, stage, G, b, N, nres, m_g,
+                                          s0_g, Mx, p.seed, rep, ep_res, p.regularize, (const Real*)p.P)) {
+      alive = false;
+      break;
+    }
+#pragma unroll
+    for (int q = 0; q < RPV; ++q) {
+      const float4 xs = snx[idx][q * RBS + t];
+      x[4 * q] = xs.x;
+      x[4 * q + 1] = xs.y;
+      x[4 * q + 2] = xs.z;
+      x[4 * q + 3] = xs.w;
+    }
+    aux1 = 0.0;
+    aux2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < RPPT; ++e) {
+      if (i0 + e < N) {
+        l[e] = lunif;
+        aux1 += (double)x[e];
+        aux2 += (double)x[e] * (double)x[e];
+      } else {
+        x[e] = 0.0f;
+        l[e] = -INFINITY;
+      }
+    }
+    PF_RMARK(5);
+    have_aux = true;
+    prev_res = true;
+    last_uniform = true;
+    F = 0.0;
+    Tprev = 0.0;
+    tstep = tv + 1;
+    vnext = s_next;  // the speculative steps after tv are discarded
   }
 
   // ---- the last step resampled: its post-resample moments -------------------
   if (alive && prev_res) {
     const double a1 = wave_sum_ud(aux1), a2 = wave_sum_ud(aux2);
+    __syncthreads();
     if (lane == 0) {
-      mslot[w][5] = a1;
-      mslot[w][6] = a2;
+      mslot[0][w][5] = a1;
+      mslot[0][w][6] = a2;
     }
     __syncthreads();
     if (t == 0) {
       double A1 = 0.0, A2 = 0.0;
       for (int j = 0; j < RNW; ++j) {
-        A1 += mslot[j][5];
-        A2 += mslot[j][6];
+        A1 += mslot[0][j][5];
+        A2 += mslot[0][j][6];
       }
       const unsigned tag = s_next + 1;
       unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
@@ -786,25 +920,25 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       const int wg = __all(good);
       if (lane == 0) okw[w] = wg;
       __syncthreads();
-      int all = 1;
+      int allg = 1;
 #pragma unroll
-      for (int j = 0; j < RCW; ++j) all &= okw[j];
-      all = __builtin_amdgcn_readfirstlane(all);
-      if (all) {
+      for (int j = 0; j < RCW; ++j) allg &= okw[j];
+      allg = __builtin_amdgcn_readfirstlane(allg);
+      if (allg) {
         if (w < RCW) {
           const double d4 = wave_sum_ud(t < G ? (double)__uint_as_float((unsigned)g5) : 0.0);
           const double d5 = wave_sum_ud(t < G ? (double)__uint_as_float((unsigned)g6) : 0.0);
           if (lane == 0) {
-            cslot[w][5] = d4;
-            cslot[w][6] = d5;
+            cslot[0][w][5] = d4;
+            cslot[0][w][6] = d5;
           }
         }
         __syncthreads();
-        if (b == 0 && t == 0) {
+        if (b == G - 1 && t == 0) {
           double S5 = 0.0, S6 = 0.0;
           for (int j = 0; j < RCW; ++j) {
-            S5 += cslot[j][5];
-            S6 += cslot[j][6];
+            S5 += cslot[0][j][5];
+            S6 += cslot[0][j][6];
           }
           const int64_t o2 = (p.T - 1) * R + r;
           const double mp = S5 / (double)N;
@@ -878,6 +1012,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
     }
   }
+#ifdef PF_STAMPS
+  if (stamp_me)
+    for (int k = 0; k < 16; ++k)
+      if (k < 6 || k > 11) g_pf_stamps[k] = racc[k];
+#endif
 }
 
 }  // namespace pf

@@ -65,7 +65,20 @@ def compare(N, T, reg=False, R=1):
           f"us/step resident {1e3 * a['ms'] / T:.2f} kstep {1e3 * b['ms'] / T:.2f}", flush=True)
 
 
+def time_only(N, T, reps=3):
+    d = S.simulate_sv_1d(T + 1, 0.95, 0.2, 1.0, seed=42)
+    Z = np.log(d.Y[1:] ** 2)
+    for _ in range(reps):
+        a = run(N, Z, d.X[0], True, T)
+        rm = np.sqrt(np.mean((a["mean"][:, 0] - d.X[1:T + 1]) ** 2))
+        print(f"{os.environ.get('PF_LIB', 'default lib')}: N={N} T={T} resident {1e3 * a['ms'] / T:.2f} us/step "
+              f"rmse {rm:.6f} resamples {int(a['flag'].sum())}", flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "time":
+        time_only(int(sys.argv[2]), int(sys.argv[3]))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "parts":
         particles_after_first_resample(int(sys.argv[2]))
         return

@@ -23,7 +23,10 @@ dev = torch.device("cuda", 0)
 dZ = torch.tensor(Z[:T, None], dtype=torch.float32, device=dev).contiguous()
 outs = [torch.zeros((T, 1), dtype=torch.float64, device=dev) for _ in range(4)]
 fl = torch.zeros((T, 1), dtype=torch.int32, device=dev)
-names = ["overhead/outputs/shift", "compute", "merge+publish", "poll", "reduce", "rollback"]
+names = ["loop top (prefetch, decision tail)", "compute", "wave partials + barrier", "publish", "verify combine",
+         "rollback (total)"]
+rb_names = {6: "rb: own tile CDF", 7: "rb: tile-sum hand-off", 8: "rb: global prefix", 9: "rb: offspring scatter",
+            10: "rb: gathered hand-off", 11: "rb: read+jitter", 12: "slow polls"}
 for rep in range(2):
     lib.pf_debug_stamps_sv_zero(16)
     NV.check(lib.pf_run_device(pf.handle, C.c_void_p(dZ.data_ptr()), None, T, 0, C.c_void_p(outs[0].data_ptr()),
@@ -38,4 +41,7 @@ for rep in range(2):
     print(f"run {rep}: steps computed {int(v[14])} rollbacks {int(v[13])} failed polls {int(v[15])} "
           f"total {tot / 100 / T:.2f} us per filter step")
     for k, n in enumerate(names):
-        print(f"   {n:24s} {v[k] / 100 / steps:8.3f} us/computed-step")
+        print(f"   {n:34s} {v[k] / 100 / steps:8.3f} us/computed-step")
+    for k, n in rb_names.items():
+        per = v[k] / 100 / max(v[13], 1) if k < 12 else v[k] / 100 / steps
+        print(f"   {n:34s} {per:8.3f} us/{'rollback' if k < 12 else 'computed-step'}")
