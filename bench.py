@@ -14,15 +14,16 @@ RCCL all-gather of every replicate's posterior summaries (means, ESS, flags),
 bracketed by barrier + device synchronisation; the max over ranks is reported.
 
 Extra JSON fields:
-  roofline      dominant kernel k_step<f32, SV> (one launch = one filter step):
-                algorithmic bytes per launch (N x 16 B: read x, lw; write x, lw —
-                SURVEY.md 8(d)) / its average device duration, timed live with HIP
-                events recorded on the engine's own stream around the timed K-step
-                run (device time / K; the run's one tail launch is charged to the
-                steps, so this slightly overstates a launch); traffic = HBM bytes
-                per launch from the committed rocprofv3 PMC passes
-                (profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 rule
-                + WRITE_SIZE), or null.
+  roofline      dominant kernel: k_resident<f32, SV> — ONE launch runs all K steps
+                with the particles register-resident (pf_resident.h); falls back to
+                k_step (one launch per step) where the resident grid does not fit.
+                achieved = algorithmic bytes per step (N x 16 B: read x, lw; write
+                x, lw — SURVEY.md 8(d)) x steps per launch / the launch's device
+                duration, timed live with HIP events recorded on the engine's own
+                stream around the timed run; traffic = HBM bytes per step from the
+                committed rocprofv3 PMC passes (profiles/pmc_traffic.json:
+                FETCH_SIZE doubled per the gfx950 rule + WRITE_SIZE), or null.  The
+                resident kernel keeps the state on chip, so traffic << algorithmic.
   cpu_baseline  the reference CPU path (faithful per-particle restatement in
                 oracle/, bit-identical to the reference) timed on this host's cores
                 on a bounded sample of the same workload.
@@ -51,14 +52,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic():
-    """HBM bytes per k_step launch from the committed PMC summary, if present."""
+def pmc_traffic(kernel):
+    """HBM bytes per filter step of `kernel` from the committed PMC summary, if present."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as fh:
         d = json.load(fh)
-    return d.get("bytes_per_launch"), d.get("source")
+    if d.get("kernel_short") != kernel:
+        return None, None
+    return d.get("bytes_per_step"), d.get("source")
 
 
 def cpu_baseline(Z, X0):
@@ -85,7 +88,6 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-launches", type=int, default=200)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,17 +176,13 @@ def main():
     allm = torch.stack(gathered).cpu().numpy()  # [world][K][3]
     rmse = [float(np.sqrt(np.mean((allm[r, :, 0] - truth) ** 2))) for r in range(world)]
 
-    # live roofline of the dominant kernel: device time of the timed run / launches
-    avg_s = device_ms * 1e-3 / K
-    # per-launch spread (one event pair per launch; the events themselves add gaps)
-    nprof = args.profile_launches
-    dZp = torch.tensor(np.resize(Zall, nprof), dtype=torch.float32, device=dev).contiguous()
-    ms = (NV.C.c_float * nprof)()
-    NV.check(lib.pf_profile_steps(pf.handle, NV.C.c_void_p(dZp.data_ptr()), nprof, ms), "pf_profile_steps")
-    durs = np.array(ms[:], dtype=float)[10:]  # drop the first launches (clock ramp)
-    alg_bytes = N_PARTICLES * 16.0
-    achieved = alg_bytes / avg_s / 1e9
-    traffic, traffic_src = pmc_traffic()
+    # live roofline of the dominant kernel: device time of the timed run
+    resident = bool(lib.pf_last_run_resident(pf.handle))
+    step_s = device_ms * 1e-3 / K
+    alg_bytes = N_PARTICLES * 16.0  # per filter step
+    achieved = alg_bytes / step_s / 1e9
+    kname = "k_resident" if resident else "k_step"
+    traffic, traffic_src = pmc_traffic(kname)
     G, tile, lds = pf.geometry()
 
     if rank == 0:
@@ -219,15 +217,21 @@ def main():
             "resample_rate": float(np.mean(allm[0, :, 2])),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "pf::k_step<float,1,1,LINEAR,LINEAR>",
-                         "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_us": avg_s * 1e6,
-                         "launches_timed": K, "traffic_source": traffic_src,
-                         "event_per_launch_us": {"median": float(np.median(durs)) * 1e3,
-                                                 "p10": float(np.percentile(durs, 10)) * 1e3,
-                                                 "p90": float(np.percentile(durs, 90)) * 1e3}},
+                         "kernel": f"pf::{kname}<float,1,1,LINEAR,LINEAR>",
+                         "steps_per_launch": K if resident else 1,
+                         "algorithmic_bytes_per_step": alg_bytes,
+                         "algorithmic_bytes_per_launch": alg_bytes * (K if resident else 1),
+                         "avg_launch_us": step_s * 1e6 * (K if resident else 1), "us_per_step": step_s * 1e6,
+                         "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    # orderly teardown: torch's wrapper of the engine stream and its events go
+    # before the engine destroys that stream (otherwise exit-time handlers can
+    # touch a destroyed stream, seen as a segfault at exit under rocprofv3)
+    del ev0, ev1, engine_stream
+    torch.cuda.synchronize()
+    pf.close()
     if dist:
         dist.destroy_process_group()
 

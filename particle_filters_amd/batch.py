@@ -69,10 +69,14 @@ class ParticleFilterBatch:
         self._h = N.C.c_void_p()
         N.check(N.load().pf_create(N.C.byref(self._desc), N.C.byref(opts), N.C.byref(self._h)), "pf_create")
 
-    def __del__(self):
+    def close(self) -> None:
+        """Release the device state now (also done on garbage collection)."""
         if N._lib is not None and getattr(self, "_h", None) is not None and self._h.value:
             N._lib.pf_destroy(self._h)
-            self._h = None
+        self._h = None
+
+    def __del__(self):
+        self.close()
 
     @property
     def handle(self):

@@ -7,6 +7,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 
 #include "pf_kernels.h"
 #include "pf_resident.h"
@@ -102,11 +103,27 @@ void register_mat_models();
 
 template <int NX, int NZ, int TK, int OK>
 struct ResidentLaunch {
+  // Every workgroup of the grid must be co-resident (they hand data to each other
+  // inside the launch).  The grid is checked against the occupancy API (one
+  // 512-thread workgroup per CU needs <= 256 VGPRs and the kernel's LDS) and
+  // launched plainly; PF_COOP=1 uses hipLaunchCooperativeKernel instead (same
+  // residency, plus the runtime's own size check).
   static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s) {
-    ResParams q = p;
-    void* args[] = {&q};
-    return hipLaunchCooperativeKernel((const void*)k_resident<float, NX, NZ, TK, OK>, dim3(G, R), dim3(RBS), args,
-                                      0, s);
+    const void* fn = (const void*)k_resident<float, NX, NZ, TK, OK>;
+    const char* coop = std::getenv("PF_COOP");
+    if (coop && std::atoi(coop) != 0) {
+      ResParams q = p;
+      void* args[] = {&q};
+      return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
+    }
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RBS, 0);
+    if (e != hipSuccess) return e;
+    if ((long long)G * R > (long long)cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
+    return hipGetLastError();
   }
 };
 
