@@ -1,29 +1,33 @@
 #!/usr/bin/env python
 """Benchmark: BASELINE config 2 — SIR filter on the 1-D SV model, N = 1e6 particles.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload sv|l96|mat]
 
 One *step* = one filter time step (predict + weight + ESS + resample-if-needed +
-posterior summary) over all N = 1,000,000 particles of one filter.  Each rank
+posterior summary) over all particles of every replicate a GPU holds.  Each rank
 (one process per GPU, ``torch.distributed`` over RCCL when N > 1) runs its own
-independent Monte-Carlo replicate (Philox replicate id = rank) on the same
-synthetic SV series; per-GPU work is fixed ("weak" scaling).  The timed region
-is W-step warm-up excluded, then exactly K steps of the device-resident loop
-(``pf_run_device``: inputs already in HBM, no host sync inside), followed by the
-RCCL all-gather of every replicate's posterior summaries (means, ESS, flags),
+independent Monte-Carlo replicates (Philox replicate ids = its global block) on
+the same synthetic series; per-GPU work is fixed ("weak" scaling).  The timed
+region is W-step warm-up excluded, then exactly K steps of the device-resident
+loop (``pf_run_device``: inputs already in HBM, no host sync inside), followed by
+the RCCL all-gather of every replicate's posterior summaries (means, ESS, flags),
 bracketed by barrier + device synchronisation; the max over ranks is reported.
 
+Workloads (BASELINE.json configs; the default is the headline metric's config):
+  sv   config 2: 1-D SV log-squared wiring, N = 1e6, one replicate per GPU
+  l96  config 3: Lorenz-96 d = 40 (RK4 g, every 4th component observed), N = 1e5
+  mat  config 4: joint 4-target acoustic tracking (nx = 16, nz = 25), N = 1e5,
+       8 replicates per GPU (64 over 8 GPUs)
+
 Extra JSON fields:
-  roofline      dominant kernel: k_resident<f32, SV> — ONE launch runs all K steps
-                with the particles register-resident (pf_resident.h); falls back to
-                k_step (one launch per step) where the resident grid does not fit.
-                achieved = algorithmic bytes per step (N x 16 B: read x, lw; write
-                x, lw — SURVEY.md 8(d)) x steps per launch / the launch's device
+  roofline      dominant kernel.  SV: k_resident<f32, SV> — ONE launch runs all K
+                steps with the particles register-resident (pf_resident.h).
+                L96/MAT: k_step (one launch per step).  achieved = algorithmic
+                bytes (N x (8 nx + 8) per replicate-step, + N x
+                (8 nx + 12) on resample steps) of the timed run / its device
                 duration, timed live with HIP events recorded on the engine's own
-                stream around the timed run; traffic = HBM bytes per step from the
-                committed rocprofv3 PMC passes (profiles/pmc_traffic.json:
-                FETCH_SIZE doubled per the gfx950 rule + WRITE_SIZE), or null.  The
-                resident kernel keeps the state on chip, so traffic << algorithmic.
+                stream; traffic = HBM bytes per step from the committed rocprofv3
+                PMC passes (profiles/pmc_traffic*.json), or null.
   cpu_baseline  the reference CPU path (faithful per-particle restatement in
                 oracle/, bit-identical to the reference) timed on this host's cores
                 on a bounded sample of the same workload.
@@ -43,7 +47,6 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "particle-steps/sec (N×T/s) + RMSE vs CPU ref, SV model N=1e6"
-N_PARTICLES = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ALPHA, SIGMA, BETA = 0.95, 0.2, 1.0
 
@@ -52,9 +55,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(workload, kernel):
     """HBM bytes per filter step of `kernel` from the committed PMC summary, if present."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    name = "pmc_traffic.json" if workload == "sv" else f"pmc_traffic_{workload}.json"
+    path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None, None
     with open(path) as fh:
@@ -64,31 +68,141 @@ def pmc_traffic(kernel):
     return d.get("bytes_per_step"), d.get("source")
 
 
-def cpu_baseline(Z, X0):
-    """Faithful reference CPU path (per-particle Python g/h, particle_filter.py:237,257)
-    on a bounded sample: the bench workload (N = 1e6) for a few steps, 1 core."""
-    from oracle import pf_oracle, ssm_oracle
+class Workload:
+    """Inputs, filter construction and CPU baseline of one BASELINE config."""
 
-    steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", "3"))
-    ssm = ssm_oracle.sv_logsq(ALPHA, SIGMA, BETA)
-    pf = pf_oracle.SIROracle(ssm.g, ssm.h, ssm.Q, ssm.R, Np=N_PARTICLES, rng=np.random.default_rng(42))
-    pf.initialize(np.array([X0]), np.array([[0.5]]))
+    name = ""
+    n_particles = 0
+    replicates = 1
+    nx = nz = 1
+    kernel_tmpl = ""
+    defaults = (1000, 100)  # steps, warmup
+
+    def build(self, T, rank):  # -> (g, h, Q, R, Z [T][nz], truth [T][nx], mean0, cov0)
+        raise NotImplementedError
+
+    def oracle_ssm(self):
+        raise NotImplementedError
+
+    def describe(self, world):
+        raise NotImplementedError
+
+
+class SV(Workload):
+    name, n_particles, replicates, nx, nz = "sv", 1_000_000, 1, 1, 1
+    kernel_tmpl = "float,1,1,LINEAR,LINEAR"
+    cpu_steps = 6
+
+    def build(self, T, rank):
+        from particle_filters_amd import models as M, simulators as S
+
+        data = S.simulate_sv_1d(T + 1, ALPHA, SIGMA, BETA, seed=42)
+        Z = np.log(data.Y[1:] ** 2)[:, None]  # log-squared wiring (PF_VS_experiments.ipynb cell 6)
+        self.X0 = data.X[0]
+        return (M.SVTransition(ALPHA), M.SVLogSqObservation(BETA), [[SIGMA ** 2]], [[M.LOGCHI2_VAR]], Z,
+                data.X[1:, None], [data.X[0]], [[0.5]])
+
+    def oracle_ssm(self):
+        from oracle import ssm_oracle
+
+        return ssm_oracle.sv_logsq(ALPHA, SIGMA, BETA)
+
+    def describe(self, world):
+        return ("SIR bootstrap PF, 1-D SV (BASELINE config 2): N=1e6 particles per GPU, "
+                "systematic resampling at Neff<0.5N, T=steps",
+                "synthetic (simulate_sv_1d alpha=0.95 sigma=0.2 beta=1 seed=42, log-squared wiring)")
+
+
+class L96(Workload):
+    name, n_particles, replicates, nx, nz = "l96", 100_000, 1, 40, 10
+    kernel_tmpl = "float,40,10,L96,LINEAR"
+    defaults = (500, 50)
+    cpu_steps = 2
+
+    def build(self, T, rank):
+        from particle_filters_amd import models as M, simulators as S
+
+        sim = S.simulate_lorenz96(nx=40, F=8.0, dt=0.01, spinup_steps=1000, total_steps=T, Np=1,
+                                  obs_interval=1, obs_fraction=4, obs_error_std=1.0, seed=42)
+        Q = 0.1 ** 2 * np.eye(40)  # the build's choice (truth is noise-free, simulator_Lorenz_96.py:394)
+        return (M.L96Transition(8.0, 0.01, 40), M.SelectObservation(sim.H_idx, 40), Q, sim.R,
+                sim.observations[1:], sim.truth_traj[1:], sim.ensemble_traj[0, 0], 2.0 * np.eye(40))
+
+    def oracle_ssm(self):
+        from oracle import ssm_oracle
+
+        return ssm_oracle.lorenz96(nx=40, q_std=0.1)
+
+    def describe(self, world):
+        return ("SIR bootstrap PF, Lorenz-96 d=40 (BASELINE config 3): RK4 dt=0.01 F=8, every 4th component "
+                "observed (R=I), Q=0.01 I, N=1e5 particles per GPU, systematic resampling at Neff<0.5N",
+                "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)")
+
+
+class MAT(Workload):
+    name, n_particles, replicates, nx, nz = "mat", 100_000, 8, 16, 25
+    kernel_tmpl = "float,16,25,LINEAR,ACOUSTIC"
+    defaults = (100, 10)
+    cpu_steps = 2
+
+    def build(self, T, rank):
+        from particle_filters_amd import models as M, simulators as S
+
+        cfg = S.ScenarioConfig(n_targets=4, n_steps=T + 1, sensor_grid_shape=(5, 5), psi=10.0, d0=0.1, seed=56,
+                               use_article_init=True)
+        data = S.simulate_acoustic_dataset(cfg, S.DynamicsConfig())
+        self.S = data["S"]
+        Qs = S.article_process_noise_cov()
+        Q = np.kron(np.eye(4), Qs)
+        R = 0.01 * np.eye(25)
+        X = data["X"].reshape(T + 1, 16)
+        return (M.CVTransition(4, 1.0), M.AcousticObservation(data["S"], 10.0, 0.1, 4), Q, R, data["Z"][1:],
+                X[1:], X[0], np.kron(np.eye(4), np.diag([100.0, 100.0, 1.0, 1.0])))
+
+    def oracle_ssm(self):
+        from oracle import ssm_oracle
+
+        return ssm_oracle.mat_joint(self.S)
+
+    def describe(self, world):
+        return (f"SIR bootstrap PF, joint 4-target acoustic tracking (BASELINE config 4): nx=16, 5x5 sensors, "
+                f"N=1e5 particles x {self.replicates} replicates per GPU ({self.replicates * world} total), "
+                "systematic resampling at Neff<0.5N",
+                "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
+
+
+WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT}
+
+
+def cpu_baseline(wl, Z, mean0, cov0):
+    """Faithful reference CPU path (per-particle Python g/h, particle_filter.py:237,257)
+    on a bounded sample: the bench workload (one replicate) for a few steps, 1 core."""
+    from oracle import pf_oracle
+
+    steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", str(wl.cpu_steps)))
+    ssm = wl.oracle_ssm()
+    pf = pf_oracle.SIROracle(ssm.g, ssm.h, ssm.Q, ssm.R, Np=wl.n_particles, rng=np.random.default_rng(42))
+    pf.initialize(np.asarray(mean0, float), np.asarray(cov0, float))
     t0 = time.perf_counter()
     for t in range(steps):
         pf.step(Z[t])
     dt = time.perf_counter() - t0
-    return {"value": N_PARTICLES * steps / dt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-            "sample": f"SV log-squared N=1e6, {steps} steps, faithful per-particle restatement "
-                      f"(oracle/pf_oracle.py, bit-identical to the reference), {dt:.1f} s"}
+    return {"value": wl.n_particles * steps / dt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{wl.name} N={wl.n_particles:.0e}, 1 replicate, {steps} steps, faithful per-particle "
+                      f"restatement (oracle/pf_oracle.py, bit-identical to the reference), {dt:.1f} s"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]()
+    K = args.steps if args.steps is not None else wl.defaults[0]
+    W = args.warmup if args.warmup is not None else wl.defaults[1]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -105,49 +219,52 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    import particle_filters_amd as pfa
-    from particle_filters_amd import _native as NV, models as M, simulators as S
+    from particle_filters_amd import _native as NV
     from particle_filters_amd.batch import ParticleFilterBatch
 
-    K, W = args.steps, args.warmup
-    data = S.simulate_sv_1d(W + K + 1, ALPHA, SIGMA, BETA, seed=42)
-    Zall = np.log(data.Y[1:] ** 2)  # log-squared wiring (PF_VS_experiments.ipynb cell 6)
+    g, h, Q, R, Zall, truth_all, mean0, cov0 = wl.build(W + K, rank)
+    nx, Rl, Np = wl.nx, wl.replicates, wl.n_particles
     dev = torch.device("cuda", local)
-    dZw = torch.tensor(Zall[:W], dtype=torch.float32, device=dev).contiguous()
-    dZ = torch.tensor(Zall[W:W + K], dtype=torch.float32, device=dev).contiguous()
 
-    pf = ParticleFilterBatch(M.SVTransition(ALPHA), M.SVLogSqObservation(BETA), [[SIGMA ** 2]],
-                             [[M.LOGCHI2_VAR]], Np=N_PARTICLES, n_replicates=1, replicate_base=rank,
+    def dz(a):  # [T][nz] shared by every replicate -> [T][R][nz] fp32 in HBM
+        a = np.broadcast_to(np.asarray(a, float)[:, None, :], (a.shape[0], Rl, wl.nz))
+        return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev).contiguous()
+
+    dZw, dZ = dz(Zall[:W]), dz(Zall[W:W + K])
+    pf = ParticleFilterBatch(g, h, Q, R, Np=Np, n_replicates=Rl, replicate_base=rank * Rl,
                              seed=42, precision="fp32", device=local)
-    pf.initialize([data.X[0]], [[0.5]])
+    pf.initialize(mean0, cov0)
     lib = NV.load()
 
     def outs(T):
-        return (torch.zeros((T, 1), dtype=torch.float64, device=dev), torch.zeros((T, 1), dtype=torch.float64, device=dev),
-                torch.zeros((T, 1), dtype=torch.int32, device=dev), torch.zeros((T, 1), dtype=torch.float64, device=dev))
+        f64 = dict(dtype=torch.float64, device=dev)
+        return (torch.zeros((T, Rl, nx), **f64), torch.zeros((T, Rl), **f64),
+                torch.zeros((T, Rl), dtype=torch.int32, device=dev), torch.zeros((T, Rl), **f64))
 
-    def run(dz, T, o):
+    def run(dzz, T, o):
         means, neff, flags, lnorm = o
-        st = lib.pf_run_device(pf.handle, NV.C.c_void_p(dz.data_ptr()), None, T, 0,
+        st = lib.pf_run_device(pf.handle, NV.C.c_void_p(dzz.data_ptr()), None, T, 0,
                                NV.C.c_void_p(means.data_ptr()), None, NV.C.c_void_p(neff.data_ptr()),
                                NV.C.c_void_p(flags.data_ptr()), NV.C.c_void_p(lnorm.data_ptr()))
         NV.check(st, "pf_run_device")
 
     ow, ot = outs(W), outs(K)
-    gathered = [torch.zeros((K, 3), dtype=torch.float64, device=dev) for _ in range(world)]
+    width = nx + 2
+    gathered = [torch.zeros((Rl, K, width), dtype=torch.float64, device=dev) for _ in range(world)]
 
     engine_stream = torch.cuda.ExternalStream(lib.pf_stream(pf.handle), device=dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-    def job(dz, T, o):
+    def job(dzz, T, o):
         """One pass of the timed sequence: T filter steps + RCCL gather of the summaries."""
         ev0.record(engine_stream)
-        run(dz, T, o)
+        run(dzz, T, o)
         ev1.record(engine_stream)
         NV.check(lib.pf_synchronize(pf.handle))
-        summary = torch.stack([o[0][:, 0], o[1][:, 0], o[2][:, 0].to(torch.float64)], dim=1)
-        if summary.shape[0] < K:
-            summary = torch.nn.functional.pad(summary, (0, 0, 0, K - summary.shape[0]))
+        summary = torch.cat([o[0], o[1][:, :, None], o[2][:, :, None].to(torch.float64)], dim=2)  # [T][R][w]
+        summary = summary.transpose(0, 1)
+        if summary.shape[1] < K:
+            summary = torch.nn.functional.pad(summary, (0, 0, 0, K - summary.shape[1]))
         if dist:
             dist.all_gather(gathered, summary.contiguous())
         else:
@@ -172,30 +289,34 @@ def main():
         elapsed = float(t.item())
 
     # posterior quality of every replicate (gathered summaries)
-    truth = data.X[W + 1:W + K + 1]
-    allm = torch.stack(gathered).cpu().numpy()  # [world][K][3]
-    rmse = [float(np.sqrt(np.mean((allm[r, :, 0] - truth) ** 2))) for r in range(world)]
+    truth = np.asarray(truth_all[W:W + K], float).reshape(K, nx)
+    allm = torch.cat(gathered).cpu().numpy()  # [world*R][K][width]
+    rmse = [float(np.sqrt(np.mean((allm[r, :, :nx] - truth) ** 2))) for r in range(allm.shape[0])]
+    local_flags = ot[2].cpu().numpy()  # [K][R] this rank's resample decisions
+    resample_rate = float(local_flags.mean())
 
     # live roofline of the dominant kernel: device time of the timed run
     resident = bool(lib.pf_last_run_resident(pf.handle))
     step_s = device_ms * 1e-3 / K
-    alg_bytes = N_PARTICLES * 16.0  # per filter step
-    achieved = alg_bytes / step_s / 1e9
+    base_b, res_b = 8.0 * nx + 8.0, 8.0 * nx + 12.0  # SURVEY.md 8(d), bytes per particle
+    alg_bytes_run = Np * (K * Rl * base_b + float(local_flags.sum()) * res_b)
+    achieved = alg_bytes_run / (device_ms * 1e-3) / 1e9
     kname = "k_resident" if resident else "k_step"
-    traffic, traffic_src = pmc_traffic(kname)
+    traffic, traffic_src = pmc_traffic(wl.name, kname)
     G, tile, lds = pf.geometry()
+    workload_desc, data_desc = wl.describe(world)
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(Zall[W:], data.X[W])
+                cpu = cpu_baseline(wl, Zall[W:], truth_all[W - 1] if W > 0 else mean0, cov0)
                 cpu["cores_on_host"] = os.cpu_count()
             except Exception as e:  # keep the bench line even if the baseline leg breaks
                 log("cpu baseline failed:", repr(e))
-        value = N_PARTICLES * K * world / elapsed
+        value = Np * Rl * K * world / elapsed
         line = {
-            "metric": METRIC,
+            "metric": METRIC if wl.name == "sv" else f"particle-steps/sec (N×T/s), {wl.name} workload",
             "value": value,
             "unit": "particle-steps/s",
             "n_gpus": world,
@@ -206,21 +327,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (simulate_sv_1d alpha=0.95 sigma=0.2 beta=1 seed=42, log-squared wiring)",
-            "config": {"workload": "SIR bootstrap PF, 1-D SV (BASELINE config 2): N=1e6 particles per GPU, "
-                                   "systematic resampling at Neff<0.5N, T=steps",
-                       "n_particles": N_PARTICLES, "replicates_per_gpu": 1,
-                       "parallelism": f"replicates x{world} (one independent filter per GPU, RCCL all-gather of summaries)",
+            "data": data_desc,
+            "config": {"workload": workload_desc, "n_particles": Np, "replicates_per_gpu": Rl,
+                       "parallelism": f"replicates x{world} (independent filters per GPU, RCCL all-gather of summaries)",
                        "geometry": {"tiles": G, "tile": tile, "lds_bytes": lds}},
             "rmse": rmse[0],
             "rmse_all_replicates": rmse,
-            "resample_rate": float(np.mean(allm[0, :, 2])),
+            "resample_rate": resample_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"pf::{kname}<float,1,1,LINEAR,LINEAR>",
+                         "kernel": f"pf::{kname}<{wl.kernel_tmpl}>",
                          "steps_per_launch": K if resident else 1,
-                         "algorithmic_bytes_per_step": alg_bytes,
-                         "algorithmic_bytes_per_launch": alg_bytes * (K if resident else 1),
+                         "algorithmic_bytes_per_step": alg_bytes_run / K,
+                         "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),
                          "avg_launch_us": step_s * 1e6 * (K if resident else 1), "us_per_step": step_s * 1e6,
                          "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src},
             "cpu_baseline": cpu,
