@@ -1,0 +1,93 @@
+"""The LEDH oracle (oracle/ledh_oracle.py) against the reference's own outputs.
+
+tests/golden/ledh_runs.npz was produced by running the reference LEDHFlowPF +
+ExtendedKalmanFilter (tests/golden/make_golden_ledh.py).  The faithful
+per-particle oracle must reproduce it bit-for-bit; the vectorised oracle (batched
+LAPACK) to fp64 rounding.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ledh_oracle as LO
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ledh_runs.npz"))
+NAMES = [str(n) for n in GOLD["names"]]
+
+
+def case(name):
+    g = {k.split("__", 1)[1]: GOLD[k] for k in GOLD.files if k.startswith(name + "__")}
+    sv = np.load(os.path.join(os.path.dirname(__file__), "golden", "sv_data.npz"))
+    mat = np.load(os.path.join(os.path.dirname(__file__), "golden", "mat_data.npz"))
+    model = {
+        "lin1d": lambda: LO.linear_1d(),
+        "lin1d_nonoise": lambda: LO.linear_1d(),
+        "sv_exp": lambda: LO.sv_exp_half(0.95, 0.2, 1.0, 0.1),
+        "acoustic": lambda: LO.acoustic_single(mat["S2"], psi=float(mat["meta2"][2]), d0=float(mat["meta2"][3])),
+        "l96": lambda: LO.lorenz96(40),
+    }[name]()
+    del sv
+    return model, g
+
+
+def run(model, g, vectorized):
+    noise = bool(g["noise"]) if "noise" in g else True
+    return LO.run_ledh(model, g["Z"], mean0=g["mean0"], cov0=g["cov0"], n_particles=int(g["n_particles"]),
+                       n_lambda_steps=int(g["n_lambda"]), ratio=float(g["ratio"]), seed=int(g["seed"]),
+                       noise=noise, vectorized=vectorized)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_faithful_oracle_bitwise(name):
+    model, g = case(name)
+    o = run(model, g, vectorized=False)
+    np.testing.assert_array_equal(o["init_particles"], g["init_particles"])
+    np.testing.assert_array_equal(o["means"], g["means"])
+    np.testing.assert_array_equal(o["covs"], g["covs"])
+    np.testing.assert_array_equal(o["final_particles"], g["particles"][-1])
+    np.testing.assert_array_equal(o["final_weights"], g["weights"][-1])
+    np.testing.assert_array_equal(o["flags"], g["flags"])
+    np.testing.assert_array_equal(o["conds"], g["conds"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_vectorized_oracle_close(name):
+    model, g = case(name)
+    o = run(model, g, vectorized=True)
+    scale = max(1.0, float(np.max(np.abs(g["means"]))))
+    np.testing.assert_allclose(o["means"], g["means"], rtol=0, atol=1e-9 * scale)
+    np.testing.assert_array_equal(o["flags"], g["flags"])
+    np.testing.assert_allclose(o["conds"], g["conds"], rtol=1e-9)
+
+
+def test_systematic_resample_matches_loop():
+    """ledh.py:25-37's loop == searchsorted(cdf, pos, 'right') (no cdf[-1]=1 fix)."""
+    rng = np.random.default_rng(3)
+    for n in (1, 7, 100, 1000):
+        w = rng.random(n) ** 4
+        U = rng.random()
+        wn = w / np.sum(w)
+        pos = (U + np.arange(n)) / n
+        cdf = np.cumsum(wn)
+        idx = np.zeros(n, dtype=int)
+        i = j = 0
+        while i < n:
+            if pos[i] < cdf[j]:
+                idx[i] = j
+                i += 1
+            else:
+                j += 1
+        np.testing.assert_array_equal(LO.systematic_resample(w, U), idx)
+
+
+def test_tracker_P_replays():
+    """The recorded tracker covariances follow from the EKF alone (not from particles)."""
+    for name in NAMES:
+        model, g = case(name)
+        tr = LO.make_ekf_tracker(model, g["mean0"], g["cov0"])
+        for t in range(len(g["Z"])):
+            _, P = tr.predict()
+            np.testing.assert_array_equal(0.5 * (P + P.T), g["tracker_P"][t])
+            tr.update(np.atleast_1d(g["Z"][t]))
