@@ -1,4 +1,5 @@
-"""ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h``).
+"""ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h`` and
+``include/pf_ledh.h``).
 
 The library is built in-tree by ``__graft_entry__.build()`` (``make -C
 particle_filters_amd/csrc``).  There is no fallback: if the library is missing
@@ -32,6 +33,11 @@ PF_RESAMPLE_SYSTEMATIC = 0
 PF_RESAMPLE_MULTINOMIAL = 1
 PF_PRECISION_FP32 = 0
 PF_PRECISION_FP64 = 1
+PF_NOISE_NONE = 0
+PF_NOISE_HOST = 1
+PF_NOISE_DEVICE = 2
+PF_LEDH_FLOW_AUTO = 0
+PF_LEDH_FLOW_PER_PARTICLE = 1
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -48,6 +54,15 @@ class Opts(C.Structure):
     _fields_ = [("n_particles", C.c_int64), ("n_replicates", C.c_int32), ("resample_method", C.c_int32),
                 ("resample_thresh", C.c_double), ("regularize", C.c_int32), ("precision", C.c_int32),
                 ("seed", C.c_uint64), ("device", C.c_int32), ("replicate_base", C.c_int32)]
+
+
+class LedhOpts(C.Structure):
+    _fields_ = [("n_particles", C.c_int64), ("n_lambda", C.c_int32), ("resample_ess_ratio", C.c_double),
+                ("seed", C.c_uint64), ("device", C.c_int32), ("flow_mode", C.c_int32)]
+
+
+class LedhInfo(C.Structure):
+    _fields_ = [("ess", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
 
 
 class UpdateInfo(C.Structure):
@@ -81,6 +96,20 @@ SIGNATURES = {
     "pf_profile_steps": (C.c_int32, [_vp, _vp, C.c_int64, C.POINTER(C.c_float)]),
     "pf_geometry": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "pf_last_run_resident": (C.c_int32, [_vp]),
+    # include/pf_ledh.h
+    "pf_ledh_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(LedhOpts), C.POINTER(_vp)]),
+    "pf_ledh_destroy": (None, [_vp]),
+    "pf_ledh_model_supported": (C.c_int32, [C.c_int32] * 4),
+    "pf_ledh_init": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp]),
+    "pf_ledh_step": (C.c_int32, [_vp, _dp, _dp, _dp, C.c_int32, _dp, C.POINTER(LedhInfo), _dp]),
+    "pf_ledh_finish": (C.c_int32, [_vp, _dp, _dp, _dp]),
+    "pf_ledh_get_particles": (C.c_int32, [_vp, _dp]),
+    "pf_ledh_get_weights": (C.c_int32, [_vp, _dp]),
+    "pf_ledh_set_state": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_ledh_run": (C.c_int32, [_vp, _dp, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp, C.POINTER(C.c_uint8)]),
+    "pf_ledh_stream": (_vp, [_vp]),
+    "pf_ledh_synchronize": (C.c_int32, [_vp]),
+    "pf_ledh_shared_path": (C.c_int32, [_vp]),
 }
 
 _lib = None

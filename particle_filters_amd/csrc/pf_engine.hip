@@ -23,6 +23,7 @@
 namespace pf {
 
 static thread_local std::string g_err;
+void set_last_error(const std::string& msg) { g_err = msg; }  // shared with pf_ledh.hip
 
 static pf_status fail(pf_status code, const std::string& msg) {
   g_err = msg;

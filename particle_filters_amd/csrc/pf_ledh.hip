@@ -1,0 +1,612 @@
+// Host side of the MI355X LEDH particle-flow filter: the C ABI of include/pf_ledh.h.
+//
+// Turns LEDHFlowPF's call sequence (/root/reference/models/LEDH_particle_filter.py:
+// init_from_gaussian 84-91, step 93-214) into launches of pf_ledh_kernels.h, and runs
+// the whole T loop on the device (pf_ledh_run) with no host synchronisation inside T.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pf_ledh.h"
+#include "pf_ledh_kernels.h"
+
+namespace pf {
+// the engine's thread-local error message (pf_last_error, pf_engine.hip)
+void set_last_error(const std::string& msg);
+namespace ledh {
+static pf_status lfail(pf_status code, const std::string& msg) {
+  set_last_error(msg);
+  return code;
+}
+
+// size (doubles) of the shared-path flow table, TLay<nx, nz>::size(L)
+static size_t TLayHost(int nx, int nz, int L) {
+  return (size_t)(nx + nz) + (size_t)L * (size_t)(nx * nz + nz * nz + nx + nz + 1);
+}
+#define LCHK(expr)                                                                          \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return lfail(PF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct LOps {
+  int nx, nz, tk, ok, psize;
+  hipError_t (*setup)(const FlowParams&, double*, int, hipStream_t);
+  hipError_t (*flow_shared)(const FlowParams&, hipStream_t);
+  hipError_t (*flow_wave)(const FlowParams&, int, hipStream_t);
+  hipError_t (*normalise_chain)(const WParams&, hipStream_t);  // tile_max, exp_sum, normalise, decide
+  hipError_t (*resample)(const WParams&, bool commit, hipStream_t);
+  hipError_t (*stats)(const WParams&, bool cov, hipStream_t);
+  hipError_t (*init)(double*, double*, const double*, const double*, const double*, int64_t, int64_t, uint64_t,
+                     uint32_t, hipStream_t);
+};
+
+template <int NX, int NZ, int TK, int OK>
+struct LL {
+  static hipError_t setup(const FlowParams& p, double* table, int L, hipStream_t s) {
+    hipLaunchKernelGGL((k_setup<NX, NZ>), dim3(L), dim3(TB), 0, s, p, table);
+    return hipGetLastError();
+  }
+  static hipError_t flow_shared(const FlowParams& p, hipStream_t s) {
+    if constexpr (OK == PF_OBS_LINEAR) {
+      hipLaunchKernelGGL((k_flow_shared<NX, NZ, TK>), dim3((unsigned)((p.N + TB - 1) / TB)), dim3(TB), 0, s, p);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
+  static hipError_t flow_wave(const FlowParams& p, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_flow_wave<NX, NZ, TK, OK>), dim3(grid), dim3(64), 0, s, p);
+    return hipGetLastError();
+  }
+  static hipError_t normalise_chain(const WParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_tile_max, dim3(p.G), dim3(TB), 0, s, p);
+    hipLaunchKernelGGL(k_exp_sum, dim3(p.G), dim3(TB), 0, s, p);
+    hipLaunchKernelGGL(k_normalise, dim3(p.G), dim3(TB), 0, s, p);
+    hipLaunchKernelGGL(k_decide, dim3(1), dim3(TB), 0, s, p, 2);
+    return hipGetLastError();
+  }
+  static hipError_t resample(const WParams& p, bool commit, hipStream_t s) {
+    const unsigned gn = (unsigned)((p.N + TB - 1) / TB);
+    hipLaunchKernelGGL(k_cdf, dim3(p.G), dim3(TB), 0, s, p, 2);
+    hipLaunchKernelGGL((k_gather<NX>), dim3(gn), dim3(TB), 0, s, p);
+    if (commit) hipLaunchKernelGGL((k_commit<NX>), dim3(gn), dim3(TB), 0, s, p);
+    return hipGetLastError();
+  }
+  static hipError_t stats(const WParams& p, bool cov, hipStream_t s) {
+    hipLaunchKernelGGL((k_mean_part<NX>), dim3(p.G), dim3(TB), 0, s, p);
+    hipLaunchKernelGGL((k_mean<NX>), dim3(1), dim3(TB), 0, s, p);
+    if (cov) {
+      hipLaunchKernelGGL((k_cov_part<NX>), dim3(p.Gc), dim3(TB), 0, s, p);
+      hipLaunchKernelGGL((k_cov<NX>), dim3(1), dim3(TB), 0, s, p);
+    }
+    return hipGetLastError();
+  }
+  static hipError_t init(double* x, double* w, const double* mean0, const double* Lc, const double* eps, int64_t N,
+                         int64_t Npad, uint64_t seed, uint32_t epoch, hipStream_t s) {
+    hipLaunchKernelGGL((k_init<NX>), dim3((unsigned)((N + TB - 1) / TB)), dim3(TB), 0, s, x, w, mean0, Lc, eps, N,
+                       Npad, seed, epoch);
+    return hipGetLastError();
+  }
+  static LOps make() {
+    LOps o;
+    o.nx = NX; o.nz = NZ; o.tk = TK; o.ok = OK;
+    o.psize = Lay<NX, NZ>::SIZE;
+    o.setup = &setup;
+    o.flow_shared = (OK == PF_OBS_LINEAR) ? &flow_shared : nullptr;
+    o.flow_wave = &flow_wave;
+    o.normalise_chain = &normalise_chain;
+    o.resample = &resample;
+    o.stats = &stats;
+    o.init = &init;
+    return o;
+  }
+};
+
+// compiled LEDH model shapes
+static const std::vector<LOps>& lregistry() {
+  static const std::vector<LOps> r = {
+      LL<1, 1, PF_TRANS_LINEAR, PF_OBS_LINEAR>::make(),      // linear 1-D (test_ledh_flow_pf.py fixtures)
+      LL<1, 1, PF_TRANS_LINEAR, PF_OBS_EXP_HALF>::make(),    // SV, h = beta exp(x/2)
+      LL<2, 1, PF_TRANS_LINEAR, PF_OBS_LINEAR>::make(),      // 2-D linear test system
+      LL<4, 9, PF_TRANS_LINEAR, PF_OBS_ACOUSTIC>::make(),    // one acoustic target, 3x3 sensors
+      LL<4, 12, PF_TRANS_LINEAR, PF_OBS_ACOUSTIC>::make(),   // one acoustic target, 3x4 sensors
+      LL<4, 25, PF_TRANS_LINEAR, PF_OBS_ACOUSTIC>::make(),   // one acoustic target, 5x5 sensors
+      LL<16, 25, PF_TRANS_LINEAR, PF_OBS_ACOUSTIC>::make(),  // joint 4-target acoustic tracking
+      LL<40, 10, PF_TRANS_L96, PF_OBS_LINEAR>::make(),       // Lorenz-96 d = 40 (BASELINE config 5)
+  };
+  return r;
+}
+static const LOps* find_lops(int nx, int nz, int tk, int ok) {
+  for (const LOps& o : lregistry())
+    if (o.nx == nx && o.nz == nz && o.tk == tk && o.ok == ok) return &o;
+  return nullptr;
+}
+
+static bool chol_lower(const double* A, int n, double jitter, std::vector<double>& L) {
+  L.assign((size_t)n * n, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = A[j * n + j] + jitter;
+    for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+    if (!(d > 0.0) || !std::isfinite(d)) return false;
+    const double ljj = std::sqrt(d);
+    L[j * n + j] = ljj;
+    for (int i = j + 1; i < n; ++i) {
+      double s = A[i * n + j];
+      for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = s / ljj;
+    }
+  }
+  return true;
+}
+
+// inverse of an SPD matrix via its Cholesky factor
+static bool spd_inverse(const double* A, int n, std::vector<double>& Ainv) {
+  std::vector<double> L;
+  if (!chol_lower(A, n, 0.0, L)) return false;
+  Ainv.assign((size_t)n * n, 0.0);
+  std::vector<double> col(n), y(n);
+  for (int c = 0; c < n; ++c) {
+    for (int i = 0; i < n; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k) s -= L[i * n + k] * y[k];
+      y[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = y[i];
+      for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * col[k];
+      col[i] = s / L[i * n + i];
+    }
+    for (int i = 0; i < n; ++i) Ainv[i * n + c] = col[i];
+  }
+  return true;
+}
+
+static bool is_diag(const double* A, int n) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      if (i != j && A[i * n + j] != 0.0) return false;
+  return true;
+}
+
+}  // namespace ledh
+}  // namespace pf
+
+using namespace pf::ledh;
+
+struct pf_ledh_handle {
+  const LOps* ops = nullptr;
+  int nx = 0, nz = 0, tk = 0, ok = 0;
+  int64_t N = 0, Npad = 0;
+  int L = 1, G = 1, Gc = 1;
+  double dlam = 1.0, ratio = 0.0;
+  uint64_t seed = 0;
+  int device = 0;
+  bool shared = false;
+  int q_diag = 0, r_diag = 0;
+  uint32_t epoch = 1;
+  bool initialized = false;
+  bool pending = false;  // the last step decided to resample
+  hipStream_t stream = nullptr;
+  std::vector<double> lams;
+  // device buffers
+  double *x = nullptr, *x_alt = nullptr, *w = nullptr, *w_alt = nullptr, *lw = nullptr;
+  double *tmax = nullptr, *tsum = nullptr, *trec = nullptr, *cdf = nullptr, *stat = nullptr, *mean = nullptr;
+  double *cpart = nullptr, *Pm = nullptr, *Pk = nullptr, *z = nullptr, *u = nullptr, *vbuf = nullptr;
+  double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
+};
+
+namespace {
+
+FlowParams flow_params(pf_ledh_handle* h, const double* Pk, const double* z, const double* u, int noise,
+                       const double* v, double* diagS) {
+  FlowParams p;
+  p.x_in = h->x;
+  p.x_out = h->x_alt;
+  p.w_in = h->w;
+  p.lw = h->lw;
+  p.Pm = h->Pm;
+  p.Pk = Pk;
+  p.z = z;
+  p.u = u;
+  p.v_host = v;
+  p.table = h->table;
+  p.lams = h->d_lams;
+  p.diagS = diagS;
+  p.N = h->N;
+  p.Npad = h->Npad;
+  p.L = h->L;
+  p.dlam = h->dlam;
+  p.noise = noise;
+  p.seed = h->seed;
+  p.epoch = h->epoch;
+  p.q_diag = h->q_diag;
+  p.r_diag = h->r_diag;
+  return p;
+}
+
+WParams w_params(pf_ledh_handle* h) {
+  WParams p;
+  p.x_in = h->x;
+  p.x_out = h->x_alt;
+  p.lw = h->lw;
+  p.w = h->w;
+  p.w_out = h->w_alt;
+  p.tmax = h->tmax;
+  p.tsum = h->tsum;
+  p.trec = h->trec;
+  p.cdf = h->cdf;
+  p.stat = h->stat;
+  p.mean = h->mean;
+  p.cpart = h->cpart;
+  p.o_mean = p.o_cov = p.o_ess = nullptr;
+  p.o_flag = nullptr;
+  p.unif = nullptr;
+  p.N = h->N;
+  p.Npad = h->Npad;
+  p.G = h->G;
+  p.Gc = h->Gc;
+  p.ratio = h->ratio;
+  p.seed = h->seed;
+  p.epoch = 0;
+  p.uniform = 0;
+  return p;
+}
+
+// flow + weights + decision of one step (ledh.py:104-203), all enqueued on h->stream
+pf_status enqueue_flow(pf_ledh_handle* h, const double* Pk, const double* z, const double* u, int noise,
+                       const double* v, double* diagS, double* o_ess, int32_t* o_flag) {
+  const uint32_t ep_noise = ++h->epoch;
+  FlowParams fp = flow_params(h, Pk, z, u, noise, v, diagS);
+  fp.epoch = ep_noise;
+  if (h->shared) {
+    LCHK(h->ops->setup(fp, h->table, h->L, h->stream));
+    LCHK(h->ops->flow_shared(fp, h->stream));
+  } else {
+    int grid = (int)std::min<int64_t>(h->N, 256 * 16);
+    LCHK(h->ops->flow_wave(fp, grid, h->stream));
+  }
+  std::swap(h->x, h->x_alt);  // the flowed particles are current
+  WParams wp = w_params(h);
+  wp.o_ess = o_ess;
+  wp.o_flag = o_flag;
+  LCHK(h->ops->normalise_chain(wp, h->stream));
+  return PF_OK;
+}
+
+// resample (flag on the device) + posterior moments of the current state
+pf_status enqueue_finish(pf_ledh_handle* h, const double* U, bool commit, double* o_mean, double* o_cov) {
+  const uint32_t ep_res = ++h->epoch;
+  WParams wp = w_params(h);
+  wp.unif = U;
+  wp.epoch = ep_res;
+  LCHK(h->ops->resample(wp, commit, h->stream));
+  WParams sp = w_params(h);
+  sp.o_mean = o_mean;
+  sp.o_cov = o_cov;
+  LCHK(h->ops->stats(sp, true, h->stream));
+  return PF_OK;
+}
+
+pf_status sym_upload(pf_ledh_handle* h, const double* P, double* dst) {
+  const int n = h->nx;
+  std::vector<double> S((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) S[i * n + j] = 0.5 * (P[i * n + j] + P[j * n + i]);  // ledh.py:106
+  LCHK(hipMemcpyAsync(dst, S.data(), S.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  LCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t pf_ledh_model_supported(int32_t nx, int32_t nz, int32_t tk, int32_t ok) {
+  return find_lops(nx, nz, tk, ok) != nullptr;
+}
+
+pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_handle** out) {
+  if (!m || !o || !out) return lfail(PF_E_ARG, "null argument");
+  *out = nullptr;
+  if (o->n_particles <= 0) return lfail(PF_E_ARG, "n_particles must be positive");
+  if (o->n_particles > (int64_t)LT * MAXT) return lfail(PF_E_ARG, "n_particles too large (max 1048576)");
+  const LOps* ops = find_lops(m->nx, m->nz, m->trans_kind, m->obs_kind);
+  if (!ops)
+    return lfail(PF_E_UNSUPPORTED, "LEDH model (nx=" + std::to_string(m->nx) + ", nz=" + std::to_string(m->nz) +
+                                       ", g=" + std::to_string(m->trans_kind) + ", h=" + std::to_string(m->obs_kind) +
+                                       ") is not compiled into libpf_hip");
+  const int nx = m->nx, nz = m->nz;
+  std::vector<double> P((size_t)ops->psize, 0.0);
+  // Lay offsets (mirrors pf_ledh_kernels.h Lay<NX, NZ>)
+  const int oA = 0, oEX = nx * nx, oH = oEX + 2, oC = oH + nz * nx, oAC = oC + nz, oLQ = oAC + 2 + 2 * nz,
+            oQI = oLQ + nx * nx, oR = oQI + nx * nx, oRI = oR + nz * nz;
+  if (m->trans_kind == PF_TRANS_LINEAR) {
+    if (m->n_trans_params < (int64_t)nx * nx || !m->trans_params) return lfail(PF_E_ARG, "LINEAR g needs A[nx*nx]");
+    for (int i = 0; i < nx * nx; ++i) P[oA + i] = m->trans_params[i];
+  } else if (m->trans_kind == PF_TRANS_L96) {
+    if (m->n_trans_params < 2 || !m->trans_params) return lfail(PF_E_ARG, "L96 g needs {F, dt}");
+    P[oEX] = m->trans_params[0];
+    P[oEX + 1] = m->trans_params[1];
+  }
+  if (m->obs_kind == PF_OBS_LINEAR) {
+    if (m->n_obs_params < (int64_t)nz * nx + nz || !m->obs_params) return lfail(PF_E_ARG, "LINEAR h needs H, c");
+    for (int i = 0; i < nz * nx; ++i) P[oH + i] = m->obs_params[i];
+    for (int i = 0; i < nz; ++i) P[oC + i] = m->obs_params[nz * nx + i];
+  } else if (m->obs_kind == PF_OBS_EXP_HALF) {
+    if (m->n_obs_params < nz || !m->obs_params) return lfail(PF_E_ARG, "EXP_HALF h needs beta[nz]");
+    for (int i = 0; i < nz; ++i) P[oC + i] = m->obs_params[i];
+  } else if (m->obs_kind == PF_OBS_ACOUSTIC) {
+    if (m->n_obs_params < 2 + 2 * nz || !m->obs_params) return lfail(PF_E_ARG, "ACOUSTIC h needs psi, d0, sx, sy");
+    for (int i = 0; i < 2 + 2 * nz; ++i) P[oAC + i] = m->obs_params[i];
+  }
+  if (!m->Q || !m->R) return lfail(PF_E_ARG, "Q and R are required");
+  std::vector<double> Lq, Qi, Ri;
+  if (!chol_lower(m->Q, nx, 0.0, Lq) && !chol_lower(m->Q, nx, 1e-10, Lq))
+    return lfail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
+  if (!spd_inverse(m->Q, nx, Qi)) return lfail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
+  if (!spd_inverse(m->R, nz, Ri)) return lfail(PF_E_NOT_PD, "Matrix is not positive definite (R)");
+  for (int i = 0; i < nx * nx; ++i) {
+    P[oLQ + i] = Lq[i];
+    P[oQI + i] = Qi[i];
+  }
+  for (int i = 0; i < nz * nz; ++i) {
+    P[oR + i] = m->R[i];
+    P[oRI + i] = Ri[i];
+  }
+  LCHK(hipSetDevice(o->device));
+  pf_ledh_handle* h = new pf_ledh_handle();
+  h->ops = ops;
+  h->nx = nx; h->nz = nz; h->tk = m->trans_kind; h->ok = m->obs_kind;
+  h->N = o->n_particles;
+  h->Npad = (h->N + 3) / 4 * 4;
+  h->L = std::max(1, (int)o->n_lambda);                   // ledh.py:132
+  h->dlam = 1.0 / (double)h->L;                           // ledh.py:133
+  double lam = 0.0;
+  for (int j = 0; j < h->L; ++j) {                        // ledh.py:134-137
+    lam = std::min(1.0, lam + h->dlam);
+    h->lams.push_back(lam);
+  }
+  h->ratio = o->resample_ess_ratio;
+  h->seed = o->seed;
+  h->device = o->device;
+  h->shared = ops->flow_shared && o->flow_mode == PF_LEDH_FLOW_AUTO;
+  h->q_diag = is_diag(Qi.data(), nx);
+  h->r_diag = is_diag(Ri.data(), nz);
+  h->G = (int)((h->N + LT - 1) / LT);
+  h->Gc = (int)((h->N + CT - 1) / CT);
+  auto bail = [&](const char* what) {
+    pf_ledh_destroy(h);
+    return lfail(PF_E_HIP, std::string("hipMalloc failed: ") + what);
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return bail("stream");
+  const size_t xb = (size_t)nx * h->Npad * sizeof(double), nb = (size_t)h->N * sizeof(double);
+  const int NP = nx * (nx + 1) / 2;
+  struct A { double** p; size_t b; };
+  A allocs[] = {{&h->x, xb}, {&h->x_alt, xb}, {&h->w, nb}, {&h->w_alt, nb}, {&h->lw, nb}, {&h->cdf, nb},
+                {&h->tmax, (size_t)h->G * 8}, {&h->tsum, (size_t)h->G * 8}, {&h->trec, (size_t)h->G * (2 + nx) * 8},
+                {&h->stat, 8 * 8}, {&h->mean, (size_t)nx * 8}, {&h->cpart, (size_t)h->Gc * NP * 8},
+                {&h->Pm, P.size() * 8}, {&h->Pk, (size_t)nx * nx * 8}, {&h->z, (size_t)nz * 8},
+                {&h->u, (size_t)nx * 8}, {&h->table, (size_t)TLayHost(nx, nz, h->L) * 8}, {&h->d_lams, (size_t)h->L * 8},
+                {&h->diagS, (size_t)h->L * nz * nz * 8}, {&h->out, (size_t)(nx + nx * nx + 2) * 8},
+                {&h->unif, 8}, {&h->Lc, (size_t)nx * nx * 8}};
+  for (auto& a : allocs)
+    if (hipMalloc((void**)a.p, a.b) != hipSuccess) return bail("state");
+  (void)hipMemset(h->x, 0, xb);
+  (void)hipMemset(h->x_alt, 0, xb);
+  if (hipMemcpy(h->Pm, P.data(), P.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->d_lams, h->lams.data(), h->lams.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return bail("upload");
+  *out = h;
+  return PF_OK;
+}
+
+void pf_ledh_destroy(pf_ledh_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean,
+                    h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc})
+    if (p) (void)hipFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+pf_status pf_ledh_init(pf_ledh_handle* h, const double* mean0, const double* cov0, const double* eps,
+                       double* mean_out, double* cov_out) {
+  if (!h || !mean0 || !cov0) return lfail(PF_E_ARG, "null argument");
+  LCHK(hipSetDevice(h->device));
+  const int nx = h->nx;
+  std::vector<double> L;
+  if (!eps && !chol_lower(cov0, nx, 0.0, L) && !chol_lower(cov0, nx, 1e-10, L))
+    return lfail(PF_E_NOT_PD, "Matrix is not positive definite (cov0)");
+  if (eps) L.assign((size_t)nx * nx, 0.0);
+  double* dm = h->out;  // staging: mean0 in out[0..nx)
+  double* deps = nullptr;
+  LCHK(hipMemcpyAsync(dm, mean0, nx * 8, hipMemcpyHostToDevice, h->stream));
+  LCHK(hipMemcpyAsync(h->Lc, L.data(), L.size() * 8, hipMemcpyHostToDevice, h->stream));
+  if (eps) {
+    if (!h->vbuf) LCHK(hipMalloc((void**)&h->vbuf, (size_t)h->N * nx * 8));
+    LCHK(hipMemcpyAsync(h->vbuf, eps, (size_t)h->N * nx * 8, hipMemcpyHostToDevice, h->stream));
+    deps = h->vbuf;
+  }
+  h->epoch = 1;
+  LCHK(h->ops->init(h->x, h->w, dm, h->Lc, deps, h->N, h->Npad, h->seed, h->epoch, h->stream));
+  // _weighted_stats of the initial set (ledh.py:90): mean -> h->mean, cov -> out[nx : nx + nx*nx)
+  WParams sp = w_params(h);
+  sp.uniform = 1;
+  sp.o_cov = h->out + nx;
+  LCHK(h->ops->stats(sp, true, h->stream));
+  LCHK(hipStreamSynchronize(h->stream));
+  if (mean_out) LCHK(hipMemcpy(mean_out, h->mean, nx * 8, hipMemcpyDeviceToHost));
+  if (cov_out) LCHK(hipMemcpy(cov_out, h->out + nx, (size_t)nx * nx * 8, hipMemcpyDeviceToHost));
+  h->initialized = true;
+  h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_ledh_step(pf_ledh_handle* h, const double* P, const double* z, const double* u, int32_t noise,
+                       const double* v, pf_ledh_info* info, double* cond_S) {
+  if (!h || !P || !z) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  if (noise == PF_NOISE_HOST && !v) return lfail(PF_E_ARG, "PF_NOISE_HOST needs v");
+  if (noise < PF_NOISE_NONE || noise > PF_NOISE_DEVICE) return lfail(PF_E_ARG, "bad noise mode");
+  LCHK(hipSetDevice(h->device));
+  if (sym_upload(h, P, h->Pk) != PF_OK) return PF_E_HIP;
+  LCHK(hipMemcpyAsync(h->z, z, h->nz * 8, hipMemcpyHostToDevice, h->stream));
+  if (u) LCHK(hipMemcpyAsync(h->u, u, h->nx * 8, hipMemcpyHostToDevice, h->stream));
+  if (noise == PF_NOISE_HOST) {
+    if (!h->vbuf) LCHK(hipMalloc((void**)&h->vbuf, (size_t)h->N * h->nx * 8));
+    LCHK(hipMemcpyAsync(h->vbuf, v, (size_t)h->N * h->nx * 8, hipMemcpyHostToDevice, h->stream));
+  }
+  pf_status st = enqueue_flow(h, h->Pk, h->z, u ? h->u : nullptr, noise, noise == PF_NOISE_HOST ? h->vbuf : nullptr,
+                              cond_S ? h->diagS : nullptr, nullptr, nullptr);
+  if (st != PF_OK) return st;
+  double stat[3];
+  LCHK(hipMemcpyAsync(stat, h->stat, 3 * 8, hipMemcpyDeviceToHost, h->stream));
+  LCHK(hipStreamSynchronize(h->stream));
+  if (cond_S) LCHK(hipMemcpy(cond_S, h->diagS, (size_t)h->L * h->nz * h->nz * 8, hipMemcpyDeviceToHost));
+  h->pending = stat[1] != 0.0;
+  if (info) {
+    info->ess = stat[0];
+    info->resample = h->pending ? 1 : 0;
+    info->_pad = 0;
+  }
+  return PF_OK;
+}
+
+pf_status pf_ledh_finish(pf_ledh_handle* h, const double* U, double* mean, double* cov) {
+  if (!h) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  LCHK(hipSetDevice(h->device));
+  const int nx = h->nx;
+  if (h->pending && U) LCHK(hipMemcpyAsync(h->unif, U, 8, hipMemcpyHostToDevice, h->stream));
+  if (h->pending) {
+    const uint32_t ep_res = ++h->epoch;
+    WParams wp = w_params(h);
+    wp.unif = U ? h->unif : nullptr;
+    wp.epoch = ep_res;
+    LCHK(h->ops->resample(wp, false, h->stream));
+    std::swap(h->x, h->x_alt);
+    std::swap(h->w, h->w_alt);
+    h->pending = false;
+  }
+  WParams sp = w_params(h);
+  sp.o_cov = h->out + nx;
+  LCHK(h->ops->stats(sp, true, h->stream));
+  LCHK(hipStreamSynchronize(h->stream));
+  if (mean) LCHK(hipMemcpy(mean, h->mean, nx * 8, hipMemcpyDeviceToHost));
+  if (cov) LCHK(hipMemcpy(cov, h->out + nx, (size_t)nx * nx * 8, hipMemcpyDeviceToHost));
+  return PF_OK;
+}
+
+pf_status pf_ledh_get_particles(pf_ledh_handle* h, double* particles) {
+  if (!h || !particles) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  LCHK(hipSetDevice(h->device));
+  std::vector<double> soa((size_t)h->nx * h->Npad);
+  LCHK(hipStreamSynchronize(h->stream));
+  LCHK(hipMemcpy(soa.data(), h->x, soa.size() * 8, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < h->N; ++i)
+    for (int d = 0; d < h->nx; ++d) particles[i * h->nx + d] = soa[(size_t)d * h->Npad + i];
+  return PF_OK;
+}
+
+pf_status pf_ledh_get_weights(pf_ledh_handle* h, double* weights) {
+  if (!h || !weights) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  LCHK(hipSetDevice(h->device));
+  LCHK(hipStreamSynchronize(h->stream));
+  LCHK(hipMemcpy(weights, h->w, (size_t)h->N * 8, hipMemcpyDeviceToHost));
+  return PF_OK;
+}
+
+pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const double* weights) {
+  if (!h || !particles || !weights) return lfail(PF_E_ARG, "null argument");
+  LCHK(hipSetDevice(h->device));
+  std::vector<double> soa((size_t)h->nx * h->Npad, 0.0);
+  for (int64_t i = 0; i < h->N; ++i)
+    for (int d = 0; d < h->nx; ++d) soa[(size_t)d * h->Npad + i] = particles[i * h->nx + d];
+  LCHK(hipStreamSynchronize(h->stream));
+  LCHK(hipMemcpy(h->x, soa.data(), soa.size() * 8, hipMemcpyHostToDevice));
+  LCHK(hipMemcpy(h->w, weights, (size_t)h->N * 8, hipMemcpyHostToDevice));
+  h->initialized = true;
+  h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T, int32_t noise,
+                      double* means, double* covs, double* ess, uint8_t* flags) {
+  if (!h || !Ps || !Z) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  if (noise != PF_NOISE_NONE && noise != PF_NOISE_DEVICE) return lfail(PF_E_ARG, "run: noise must be NONE or DEVICE");
+  if (T <= 0) return PF_OK;
+  LCHK(hipSetDevice(h->device));
+  const int nx = h->nx, nz = h->nz;
+  std::vector<double> S((size_t)T * nx * nx);
+  for (int64_t t = 0; t < T; ++t)
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nx; ++j)
+        S[(t * nx + i) * nx + j] = 0.5 * (Ps[(t * nx + i) * nx + j] + Ps[(t * nx + j) * nx + i]);
+  double *dP = nullptr, *dZ = nullptr, *dU = nullptr, *dm = nullptr, *dc = nullptr, *de = nullptr;
+  int32_t* df = nullptr;
+  auto cleanup = [&]() {
+    for (double* p : {dP, dZ, dU, dm, dc, de})
+      if (p) (void)hipFree(p);
+    if (df) (void)hipFree(df);
+  };
+  bool ok = hipMalloc((void**)&dP, S.size() * 8) == hipSuccess && hipMalloc((void**)&dZ, (size_t)T * nz * 8) == hipSuccess &&
+            (!U || hipMalloc((void**)&dU, (size_t)T * nx * 8) == hipSuccess) &&
+            hipMalloc((void**)&dm, (size_t)T * nx * 8) == hipSuccess &&
+            hipMalloc((void**)&dc, (size_t)T * nx * nx * 8) == hipSuccess &&
+            hipMalloc((void**)&de, (size_t)T * 8) == hipSuccess && hipMalloc((void**)&df, (size_t)T * 4) == hipSuccess;
+  if (!ok) {
+    cleanup();
+    return lfail(PF_E_HIP, "hipMalloc of run buffers failed");
+  }
+  pf_status st = PF_OK;
+  do {
+    if (hipMemcpyAsync(dP, S.data(), S.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+        hipMemcpyAsync(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+        (U && hipMemcpyAsync(dU, U, (size_t)T * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)) {
+      st = lfail(PF_E_HIP, "upload of run inputs failed");
+      break;
+    }
+    for (int64_t t = 0; t < T && st == PF_OK; ++t) {
+      st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
+                        df + t);
+      if (st == PF_OK) st = enqueue_finish(h, nullptr, true, dm + t * nx, dc + t * nx * nx);
+    }
+    if (st != PF_OK) break;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) {
+      st = lfail(PF_E_HIP, "run: stream synchronisation failed");
+      break;
+    }
+    std::vector<int32_t> fl((size_t)T);
+    if ((means && hipMemcpy(means, dm, (size_t)T * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (covs && hipMemcpy(covs, dc, (size_t)T * nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (ess && hipMemcpy(ess, de, (size_t)T * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        hipMemcpy(fl.data(), df, (size_t)T * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+      st = lfail(PF_E_HIP, "download of run outputs failed");
+      break;
+    }
+    if (flags)
+      for (int64_t t = 0; t < T; ++t) flags[t] = fl[t] ? 1 : 0;
+  } while (false);
+  cleanup();
+  h->pending = false;
+  return st;
+}
+
+void* pf_ledh_stream(pf_ledh_handle* h) { return h ? (void*)h->stream : nullptr; }
+pf_status pf_ledh_synchronize(pf_ledh_handle* h) {
+  if (!h) return lfail(PF_E_ARG, "null argument");
+  LCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+int32_t pf_ledh_shared_path(pf_ledh_handle* h) { return (h && h->shared) ? 1 : 0; }
+
+}  // extern "C"

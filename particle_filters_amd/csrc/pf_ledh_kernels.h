@@ -1,0 +1,1049 @@
+// LEDH particle-flow kernels for gfx950 (fp64, wave64).
+//
+// The reference's LEDHFlowPF.step (/root/reference/models/LEDH_particle_filter.py,
+// "ledh.py:LINE") linearises h at every particle for every pseudo-time step
+// lambda_j and forms dense nx x nx matrices per particle:
+//   S = lam H P H^T + R,  A = -1/2 P H^T S^{-1} H,  b = (I + 2 lam A)[(I + lam A) P H^T R^{-1}(z - e) + A eta0]
+//   eta += dlam (A eta + b),  theta += log|det(I + dlam A)|                        (ledh.py:136-179)
+// Here the same quantities are evaluated in observation space, never forming A:
+//   K = P H^T (nx x nz), M = H K, Gm = -1/2 K S^{-1}  =>  A v = Gm (H v),
+//   det(I + dlam A) = det(S - dlam/2 M) / det(S)      (matrix-determinant lemma;
+//   the reference's +1e-12 I retry becomes (1+eps)^nx det(S - dlam/(2(1+eps)) M) / det(S)).
+// That is O(nx nz^2 + nz^3) per particle and lambda instead of O(nx^3).
+//
+// Two flow kernels:
+//   k_flow_shared  h linear (L96 x[::k], linear test systems): H, e = c, and hence K, M, S, Gm,
+//                  the logdets and P H^T R^{-1}(z - e) are the SAME for every particle.
+//                  k_setup computes them once per lambda_j (one workgroup per j) into a
+//                  table; a particle then only carries observation-space vectors:
+//                  y = H eta, s_j = y + y0 + 2 lam_j H w_j, eta_L = eta0 + sum_j dlam (c + lam_j ac_j + Gm_j s_j).
+//                  One thread per particle, SoA loads/stores.
+//   k_flow_wave    any h with an analytic Jacobian (EXP_HALF, ACOUSTIC): one 64-lane
+//                  workgroup per particle (persistent over particles), the small dense
+//                  algebra in LDS with lanes over matrix entries.
+// Both end in the weight of ledh.py:186-190:
+//   l_i = log(w_i + 1e-300) + theta_i + log N(eta_i; g(x_i), Q) + log N(z; h(eta_i), R) - log N(eta0_i; g(x_i), Q)
+// (the Gaussian normalising constants cancel between numerator and denominator, and
+// across particles in the normalisation, so they are not evaluated).
+//
+// Then the weight pipeline (tiles of LT particles, fixed-order reductions so every
+// workgroup derives bit-identical global scalars):
+//   k_tile_max -> k_exp_sum -> k_normalise (w, tile sums of w, w^2, w x) -> k_decide (ESS,
+//   resample flag) -> [k_cdf -> k_gather] (systematic, ledh.py:25-37, 204-206) ->
+//   k_mean_part -> k_mean -> k_cov_part -> k_cov (ledh.py:217-224).
+//
+// Layout in HBM: particles SoA x[nx][Npad] (fp64), weights w[N] (normalised, ledh.py:195).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pf_ledh.h"
+#include "philox.h"
+
+namespace pf {
+namespace ledh {
+
+constexpr int TB = 256;    // block of the per-particle-thread and reduction kernels
+constexpr int LT = 1024;   // particles per reduction tile
+constexpr int MAXT = 1024; // tiles (N <= LT * MAXT)
+constexpr int CT = 128;    // particles per covariance tile
+
+// ---------------------------------------------------------------------------
+// parameter layout (doubles)
+// ---------------------------------------------------------------------------
+template <int NX, int NZ>
+struct Lay {
+  static constexpr int A = 0;                 // NX*NX transition matrix (LINEAR g)
+  static constexpr int EX = A + NX * NX;      // F, dt (L96 g)
+  static constexpr int H = EX + 2;            // NZ*NX observation matrix (LINEAR h)
+  static constexpr int C = H + NZ * NX;       // NZ offset (LINEAR) / beta (EXP_HALF)
+  static constexpr int AC = C + NZ;           // psi, d0, sx[NZ], sy[NZ] (ACOUSTIC)
+  static constexpr int LQ = AC + 2 + 2 * NZ;  // NX*NX chol(Q) (device noise)
+  static constexpr int QI = LQ + NX * NX;     // NX*NX Q^{-1}
+  static constexpr int R = QI + NX * NX;      // NZ*NZ R
+  static constexpr int RI = R + NZ * NZ;      // NZ*NZ R^{-1}
+  static constexpr int SIZE = RI + NZ * NZ;
+};
+
+// shared-path flow table (doubles)
+template <int NX, int NZ>
+struct TLay {
+  static constexpr int Cv = 0;               // NX  c = K R^{-1}(z - e)   (= P H^T R^{-1}(z - e), ledh.py:163-164)
+  static constexpr int HC = Cv + NX;         // NZ  H c
+  static constexpr int HEAD = HC + NZ;
+  static constexpr int GM = 0;               // NX*NZ  Gm_j = -1/2 K S_j^{-1}
+  static constexpr int HGM = GM + NX * NZ;   // NZ*NZ  H Gm_j
+  static constexpr int AC = HGM + NZ * NZ;   // NX     A_j c = Gm_j H c
+  static constexpr int HAC = AC + NX;        // NZ     H A_j c
+  static constexpr int LD = HAC + NZ;        // 1      log|det(I + dlam A_j)|
+  static constexpr int PJ = LD + 1;
+  static constexpr int size(int L) { return HEAD + L * PJ; }
+};
+
+struct FlowParams {
+  const double* x_in;   // [NX][Npad]
+  double* x_out;        // [NX][Npad]
+  const double* w_in;   // [N] normalised weights
+  double* lw;           // [N] unnormalised log weights (out)
+  const double* Pm;     // Lay
+  const double* Pk;     // [NX][NX] symmetrised tracker covariance
+  const double* z;      // [NZ]
+  const double* u;      // [NX] or null
+  const double* v_host; // [N][NX] or null
+  const double* table;  // TLay (shared path)
+  const double* lams;   // [L]
+  double* diagS;        // [L][NZ][NZ] or null (S of particle 0)
+  int64_t N, Npad;
+  int L;
+  double dlam;
+  int noise;
+  uint64_t seed;
+  uint32_t epoch;
+  int q_diag, r_diag;
+};
+
+// ---------------------------------------------------------------------------
+// model pieces
+// ---------------------------------------------------------------------------
+template <int NX>
+__device__ __forceinline__ double l96_rhs_at(const double* x, int a, double F) {
+  return (x[(a + 1) % NX] - x[(a + NX - 2) % NX]) * x[(a + NX - 1) % NX] - x[a] + F;
+}
+
+// g(x, u) for one particle in registers (thread path)
+template <int NX, int NZ, int TK>
+__device__ __forceinline__ void g_thread(double* x, const double* __restrict__ Pm, const double* u) {
+  using L = Lay<NX, NZ>;
+  if constexpr (TK == PF_TRANS_LINEAR) {
+    double y[NX];
+#pragma unroll
+    for (int d = 0; d < NX; ++d) {
+      double acc = 0.0;
+#pragma unroll
+      for (int e = 0; e < NX; ++e) acc += Pm[L::A + d * NX + e] * x[e];
+      y[d] = acc;
+    }
+#pragma unroll
+    for (int d = 0; d < NX; ++d) x[d] = u ? y[d] + u[d] : y[d];
+  } else {  // L96: x + dt/6 (k1 + 2 k2 + 2 k3 + k4)  (simulator_Lorenz_96.py:62-84)
+    const double F = Pm[L::EX], dt = Pm[L::EX + 1];
+    double k[NX], acc[NX], tmp[NX];
+#pragma unroll
+    for (int a = 0; a < NX; ++a) k[a] = l96_rhs_at<NX>(x, a, F);
+#pragma unroll
+    for (int a = 0; a < NX; ++a) { acc[a] = k[a]; tmp[a] = x[a] + 0.5 * dt * k[a]; }
+#pragma unroll
+    for (int a = 0; a < NX; ++a) k[a] = l96_rhs_at<NX>(tmp, a, F);
+#pragma unroll
+    for (int a = 0; a < NX; ++a) { acc[a] += 2.0 * k[a]; }
+#pragma unroll
+    for (int a = 0; a < NX; ++a) tmp[a] = x[a] + 0.5 * dt * k[a];
+#pragma unroll
+    for (int a = 0; a < NX; ++a) k[a] = l96_rhs_at<NX>(tmp, a, F);
+#pragma unroll
+    for (int a = 0; a < NX; ++a) { acc[a] += 2.0 * k[a]; tmp[a] = x[a] + dt * k[a]; }
+#pragma unroll
+    for (int a = 0; a < NX; ++a) k[a] = l96_rhs_at<NX>(tmp, a, F);
+    const double h6 = dt / 6.0;
+#pragma unroll
+    for (int a = 0; a < NX; ++a) x[a] = x[a] + h6 * (acc[a] + k[a]);
+    if (u) {
+#pragma unroll
+      for (int a = 0; a < NX; ++a) x[a] += u[a];
+    }
+  }
+}
+
+// process noise of particle i (thread path): v = chol(Q) n, n ~ Philox, or the host draw
+template <int NX, int NZ>
+__device__ __forceinline__ void noise_thread(const FlowParams& p, int64_t i, double* v) {
+  using L = Lay<NX, NZ>;
+  if (p.noise == PF_NOISE_HOST) {
+#pragma unroll
+    for (int d = 0; d < NX; ++d) v[d] = p.v_host[i * NX + d];
+  } else if (p.noise == PF_NOISE_DEVICE) {
+    double n[NX];
+#pragma unroll
+    for (int d = 0; d < NX; ++d) {
+      const int64_t f = i * NX + d;
+      n[d] = normal4<double>(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS).v[f & 3];
+    }
+#pragma unroll
+    for (int d = 0; d < NX; ++d) {
+      double acc = 0.0;
+#pragma unroll
+      for (int e = 0; e <= d; ++e) acc += p.Pm[L::LQ + d * NX + e] * n[e];
+      v[d] = acc;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < NX; ++d) v[d] = 0.0;
+  }
+}
+
+// d^T C d for C = Q^{-1} (NX) or R^{-1} (NZ), row-major at Pm[off]
+template <int D>
+__device__ __forceinline__ double quad_form(const double* d, const double* __restrict__ C, bool diag) {
+  double q = 0.0;
+  if (diag) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) q += d[a] * (C[a * D + a] * d[a]);
+  } else {
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      double t = 0.0;
+#pragma unroll
+      for (int b = 0; b < D; ++b) t += C[a * D + b] * d[b];
+      q += d[a] * t;
+    }
+  }
+  return q;
+}
+
+// ---------------------------------------------------------------------------
+// block-level small dense algebra in LDS (row-major, no pivoting: S, S - c M are SPD)
+// ---------------------------------------------------------------------------
+// Gauss-Jordan on aug [n][2n] = [S | I] -> [I | S^{-1}]; returns log|det S| and its sign.
+__device__ __forceinline__ void block_gauss_jordan(double* aug, int n, double* fac, double* logabs, int* sign) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int w = 2 * n;
+  double la = 0.0;
+  int sg = 1;
+  for (int p = 0; p < n; ++p) {
+    const double piv = aug[p * w + p];
+    la += log(fabs(piv));
+    if (piv < 0.0) sg = -sg;
+    if (piv == 0.0) sg = 0;
+    for (int r = t; r < n; r += nt) fac[r] = aug[r * w + p];
+    __syncthreads();
+    for (int c = t; c < w; c += nt) aug[p * w + c] = aug[p * w + c] / piv;
+    __syncthreads();
+    for (int q = t; q < n * w; q += nt) {
+      const int r = q / w, c = q - r * w;
+      if (r != p) aug[q] = aug[q] - fac[r] * aug[p * w + c];
+    }
+    __syncthreads();
+  }
+  *logabs = la;
+  *sign = sg;
+}
+
+// LU elimination (no pivoting) of T [n][n] in place; log|det| and sign.
+__device__ __forceinline__ void block_logdet(double* T, int n, double* fac, double* logabs, int* sign) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  double la = 0.0;
+  int sg = 1;
+  for (int p = 0; p < n; ++p) {
+    const double piv = T[p * n + p];
+    la += log(fabs(piv));
+    if (piv < 0.0) sg = -sg;
+    if (piv == 0.0) sg = 0;
+    for (int r = p + 1 + t; r < n; r += nt) fac[r] = T[r * n + p] / piv;
+    __syncthreads();
+    const int m = n - p - 1;
+    for (int q = t; q < m * m; q += nt) {
+      const int r = p + 1 + q / m, c = p + 1 + q % m;
+      T[r * n + c] = T[r * n + c] - fac[r] * T[p * n + c];
+    }
+    __syncthreads();
+  }
+  *logabs = la;
+  *sign = sg;
+}
+
+// log|det(I + dlam A)| = log|det(S - dlam/2 M)| - log|det S|, with the reference's
+// +1e-12 I retry (ledh.py:174-179) when that determinant is not positive.
+// S_ld/S_sg: log|det S| and sign; M, R: LDS matrices; T, fac scratch.
+template <int NX, int NZ>
+__device__ __forceinline__ double flow_logdet(const double* M, const double* R, double lam, double dlam, double S_ld,
+                                              int S_sg, double* T, double* fac) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const double c1 = lam - 0.5 * dlam;
+  for (int q = t; q < NZ * NZ; q += nt) T[q] = c1 * M[q] + R[q];
+  __syncthreads();
+  double ld;
+  int sg;
+  block_logdet(T, NZ, fac, &ld, &sg);
+  if (sg * S_sg > 0) return ld - S_ld;
+  const double eps = 1e-12;
+  const double c2 = lam - dlam / (2.0 * (1.0 + eps));
+  for (int q = t; q < NZ * NZ; q += nt) T[q] = c2 * M[q] + R[q];
+  __syncthreads();
+  block_logdet(T, NZ, fac, &ld, &sg);
+  return (double)NX * log1p(eps) + ld - S_ld;
+}
+
+// ---------------------------------------------------------------------------
+// k_setup: the shared-path table, one workgroup per lambda step j
+// ---------------------------------------------------------------------------
+template <int NX, int NZ>
+struct SetupSmem {
+  static constexpr int P = 0;                 // NX*NX
+  static constexpr int H = P + NX * NX;       // NZ*NX
+  static constexpr int K = H + NZ * NX;       // NX*NZ
+  static constexpr int M = K + NX * NZ;       // NZ*NZ
+  static constexpr int R = M + NZ * NZ;       // NZ*NZ
+  static constexpr int AUG = R + NZ * NZ;     // NZ*2NZ
+  static constexpr int T = AUG + 2 * NZ * NZ; // NZ*NZ
+  static constexpr int GM = T + NZ * NZ;      // NX*NZ
+  static constexpr int RV = GM + NX * NZ;     // NZ   R^{-1}(z - e)
+  static constexpr int CV = RV + NZ;          // NX   c
+  static constexpr int HC = CV + NX;          // NZ
+  static constexpr int AC = HC + NZ;          // NX
+  static constexpr int FAC = AC + NX;         // NZ
+  static constexpr int SIZE = FAC + NZ;
+};
+
+template <int NX, int NZ>
+__global__ void __launch_bounds__(TB) k_setup(FlowParams p, double* table) {
+  using L = Lay<NX, NZ>;
+  using T = TLay<NX, NZ>;
+  using SM = SetupSmem<NX, NZ>;
+  __shared__ double sm[SM::SIZE];
+  const int t = threadIdx.x, j = blockIdx.x;
+  const double* __restrict__ Pm = p.Pm;
+  for (int q = t; q < NX * NX; q += TB) sm[SM::P + q] = p.Pk[q];
+  for (int q = t; q < NZ * NX; q += TB) sm[SM::H + q] = Pm[L::H + q];
+  for (int q = t; q < NZ * NZ; q += TB) sm[SM::R + q] = Pm[L::R + q];
+  __syncthreads();
+  // K = P H^T
+  for (int q = t; q < NX * NZ; q += TB) {
+    const int d = q / NZ, k = q - d * NZ;
+    double acc = 0.0;
+    for (int e = 0; e < NX; ++e) acc += sm[SM::P + d * NX + e] * sm[SM::H + k * NX + e];
+    sm[SM::K + q] = acc;
+  }
+  // r = R^{-1} (z - e), e = h(eta) - H eta = c for a linear h
+  for (int k = t; k < NZ; k += TB) {
+    double acc = 0.0;
+    for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - Pm[L::C + l]);
+    sm[SM::RV + k] = acc;
+  }
+  __syncthreads();
+  // M = H K ; c = K r
+  for (int q = t; q < NZ * NZ; q += TB) {
+    const int k = q / NZ, l = q - k * NZ;
+    double acc = 0.0;
+    for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::K + d * NZ + l];
+    sm[SM::M + q] = acc;
+  }
+  for (int d = t; d < NX; d += TB) {
+    double acc = 0.0;
+    for (int k = 0; k < NZ; ++k) acc += sm[SM::K + d * NZ + k] * sm[SM::RV + k];
+    sm[SM::CV + d] = acc;
+  }
+  __syncthreads();
+  for (int k = t; k < NZ; k += TB) {
+    double acc = 0.0;
+    for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::CV + d];
+    sm[SM::HC + k] = acc;
+  }
+  const double lam = p.lams[j];
+  // S = lam M + R -> [S | I]
+  for (int q = t; q < NZ * 2 * NZ; q += TB) {
+    const int r = q / (2 * NZ), c = q - r * 2 * NZ;
+    sm[SM::AUG + q] = c < NZ ? lam * sm[SM::M + r * NZ + c] + sm[SM::R + r * NZ + c] : (c - NZ == r ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  if (p.diagS)
+    for (int q = t; q < NZ * NZ; q += TB) p.diagS[(int64_t)j * NZ * NZ + q] = sm[SM::AUG + (q / NZ) * 2 * NZ + q % NZ];
+  __syncthreads();
+  double S_ld;
+  int S_sg;
+  block_gauss_jordan(sm + SM::AUG, NZ, sm + SM::FAC, &S_ld, &S_sg);
+  const double ld = flow_logdet<NX, NZ>(sm + SM::M, sm + SM::R, lam, p.dlam, S_ld, S_sg, sm + SM::T, sm + SM::FAC);
+  // Gm = -1/2 K S^{-1}
+  for (int q = t; q < NX * NZ; q += TB) {
+    const int d = q / NZ, l = q - d * NZ;
+    double acc = 0.0;
+    for (int k = 0; k < NZ; ++k) acc += sm[SM::K + d * NZ + k] * sm[SM::AUG + k * 2 * NZ + NZ + l];
+    sm[SM::GM + q] = -0.5 * acc;
+  }
+  __syncthreads();
+  double* tj = table + T::HEAD + (int64_t)j * T::PJ;
+  for (int d = t; d < NX; d += TB) {
+    double acc = 0.0;
+    for (int l = 0; l < NZ; ++l) acc += sm[SM::GM + d * NZ + l] * sm[SM::HC + l];
+    sm[SM::AC + d] = acc;
+    tj[T::AC + d] = acc;
+  }
+  for (int q = t; q < NX * NZ; q += TB) tj[T::GM + q] = sm[SM::GM + q];
+  __syncthreads();
+  for (int q = t; q < NZ * NZ; q += TB) {
+    const int k = q / NZ, l = q - k * NZ;
+    double acc = 0.0;
+    for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::GM + d * NZ + l];
+    tj[T::HGM + q] = acc;
+  }
+  for (int k = t; k < NZ; k += TB) {
+    double acc = 0.0;
+    for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::AC + d];
+    tj[T::HAC + k] = acc;
+  }
+  if (t == 0) tj[T::LD] = ld;
+  if (j == 0) {
+    for (int d = t; d < NX; d += TB) table[T::Cv + d] = sm[SM::CV + d];
+    for (int k = t; k < NZ; k += TB) table[T::HC + k] = sm[SM::HC + k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_flow_shared: one thread per particle (linear h)
+// ---------------------------------------------------------------------------
+template <int NX, int NZ, int TK>
+__global__ void __launch_bounds__(TB) k_flow_shared(FlowParams p) {
+  using L = Lay<NX, NZ>;
+  using T = TLay<NX, NZ>;
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (i >= p.N) return;
+  const double* __restrict__ Pm = p.Pm;
+  const double* __restrict__ tb = p.table;
+  double x[NX];
+#pragma unroll
+  for (int d = 0; d < NX; ++d) x[d] = p.x_in[(int64_t)d * p.Npad + i];
+  g_thread<NX, NZ, TK>(x, Pm, p.u);  // x <- g(x_{k-1}, u)
+  double v[NX];
+  noise_thread<NX, NZ>(p, i, v);
+  // eta0 = g(x) + v, parked in x_out (re-read at the end)
+  double y0[NZ];
+#pragma unroll
+  for (int k = 0; k < NZ; ++k) y0[k] = 0.0;
+#pragma unroll
+  for (int d = 0; d < NX; ++d) {
+    const double e0 = x[d] + v[d];
+    p.x_out[(int64_t)d * p.Npad + i] = e0;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) y0[k] += Pm[L::H + k * NX + d] * e0;
+  }
+  const double den = quad_form<NX>(v, Pm + L::QI, p.q_diag != 0);
+  double y[NZ], delta[NX];
+#pragma unroll
+  for (int k = 0; k < NZ; ++k) y[k] = y0[k];
+#pragma unroll
+  for (int d = 0; d < NX; ++d) delta[d] = 0.0;
+  double theta = 0.0;
+  const double dlam = p.dlam;
+  for (int j = 0; j < p.L; ++j) {
+    const double lam = p.lams[j];
+    const double* tj = tb + T::HEAD + (int64_t)j * T::PJ;
+    double s[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+      double hw = tb[T::HC + k] + lam * tj[T::HAC + k];
+#pragma unroll
+      for (int l = 0; l < NZ; ++l) hw += tj[T::HGM + k * NZ + l] * y0[l];
+      s[k] = y[k] + y0[k] + 2.0 * lam * hw;
+    }
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+      double q = tb[T::HC + k] + lam * tj[T::HAC + k];
+#pragma unroll
+      for (int l = 0; l < NZ; ++l) q += tj[T::HGM + k * NZ + l] * s[l];
+      y[k] += dlam * q;
+    }
+#pragma unroll
+    for (int d = 0; d < NX; ++d) {
+      double q = tb[T::Cv + d] + lam * tj[T::AC + d];
+#pragma unroll
+      for (int l = 0; l < NZ; ++l) q += tj[T::GM + d * NZ + l] * s[l];
+      delta[d] += dlam * q;
+    }
+    theta += tj[T::LD];
+  }
+  // eta = eta0 + delta; eta - g(x) = v + delta
+#pragma unroll
+  for (int d = 0; d < NX; ++d) {
+    const int64_t o = (int64_t)d * p.Npad + i;
+    p.x_out[o] = p.x_out[o] + delta[d];
+    v[d] += delta[d];
+  }
+  const double num_t = quad_form<NX>(v, Pm + L::QI, p.q_diag != 0);
+  double ez[NZ];
+#pragma unroll
+  for (int k = 0; k < NZ; ++k) ez[k] = p.z[k] - (y[k] + Pm[L::C + k]);
+  const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
+  const double lw0 = log(p.w_in[i] + 1e-300) + theta;
+  p.lw[i] = lw0 + ((-0.5 * num_t) + (-0.5 * like) - (-0.5 * den));
+}
+
+// ---------------------------------------------------------------------------
+// k_flow_wave: one 64-lane workgroup per particle, any h with a Jacobian
+// ---------------------------------------------------------------------------
+template <int NX, int NZ>
+struct WaveSmem {
+  static constexpr int P = 0;                 // NX*NX
+  static constexpr int R = P + NX * NX;       // NZ*NZ
+  static constexpr int XP = R + NZ * NZ;      // NX  x_{k-1}
+  static constexpr int GX = XP + NX;          // NX  g(x)
+  static constexpr int V = GX + NX;           // NX  v (noise), later scratch
+  static constexpr int E0 = V + NX;           // NX  eta0
+  static constexpr int ET = E0 + NX;          // NX  eta
+  static constexpr int T1 = ET + NX;          // NX
+  static constexpr int T2 = T1 + NX;          // NX
+  static constexpr int CV = T2 + NX;          // NX  c
+  static constexpr int H = CV + NX;           // NZ*NX
+  static constexpr int K = H + NZ * NX;       // NX*NZ
+  static constexpr int M = K + NX * NZ;       // NZ*NZ
+  static constexpr int AUG = M + NZ * NZ;     // NZ*2NZ
+  static constexpr int TT = AUG + 2 * NZ * NZ;// NZ*NZ
+  static constexpr int GM = TT + NZ * NZ;     // NX*NZ
+  static constexpr int HV = GM + NX * NZ;     // NZ  h(eta)
+  static constexpr int ZE = HV + NZ;          // NZ  e / scratch
+  static constexpr int ZT = ZE + NZ;          // NZ  scratch
+  static constexpr int FAC = ZT + NZ;         // NZ
+  static constexpr int RED = FAC + NZ;        // 64
+  static constexpr int SIZE = RED + 64;
+};
+
+template <int NX, int NZ, int TK>
+__device__ __forceinline__ void g_block(const double* x, double* out, double* tmp, double* kk, const double* __restrict__ Pm,
+                                        const double* u) {
+  using L = Lay<NX, NZ>;
+  const int t = threadIdx.x;
+  if constexpr (TK == PF_TRANS_LINEAR) {
+    for (int d = t; d < NX; d += blockDim.x) {
+      double acc = 0.0;
+      for (int e = 0; e < NX; ++e) acc += Pm[L::A + d * NX + e] * x[e];
+      out[d] = u ? acc + u[d] : acc;
+    }
+    __syncthreads();
+  } else {
+    const double F = Pm[L::EX], dt = Pm[L::EX + 1];
+    // out accumulates k1 + 2k2 + 2k3; kk holds the current stage slope
+    for (int a = t; a < NX; a += blockDim.x) { kk[a] = l96_rhs_at<NX>(x, a, F); out[a] = kk[a]; tmp[a] = x[a] + 0.5 * dt * kk[a]; }
+    __syncthreads();
+    for (int a = t; a < NX; a += blockDim.x) kk[a] = l96_rhs_at<NX>(tmp, a, F);
+    __syncthreads();
+    for (int a = t; a < NX; a += blockDim.x) { out[a] += 2.0 * kk[a]; tmp[a] = x[a] + 0.5 * dt * kk[a]; }
+    __syncthreads();
+    for (int a = t; a < NX; a += blockDim.x) kk[a] = l96_rhs_at<NX>(tmp, a, F);
+    __syncthreads();
+    for (int a = t; a < NX; a += blockDim.x) { out[a] += 2.0 * kk[a]; tmp[a] = x[a] + dt * kk[a]; }
+    __syncthreads();
+    for (int a = t; a < NX; a += blockDim.x) kk[a] = l96_rhs_at<NX>(tmp, a, F);
+    __syncthreads();
+    const double h6 = dt / 6.0;
+    for (int a = t; a < NX; a += blockDim.x) {
+      const double r = x[a] + h6 * (out[a] + kk[a]);
+      out[a] = u ? r + u[a] : r;
+    }
+    __syncthreads();
+  }
+}
+
+// H = dh/deta and h(eta) at eta (LDS), lanes over entries
+template <int NX, int NZ, int OK>
+__device__ __forceinline__ void obs_jac_block(const double* eta, double* H, double* hv, const double* __restrict__ Pm) {
+  using L = Lay<NX, NZ>;
+  const int t = threadIdx.x;
+  if constexpr (OK == PF_OBS_LINEAR) {
+    for (int q = t; q < NZ * NX; q += blockDim.x) H[q] = Pm[L::H + q];
+    for (int k = t; k < NZ; k += blockDim.x) {
+      double acc = 0.0;
+      for (int e = 0; e < NX; ++e) acc += Pm[L::H + k * NX + e] * eta[e];
+      hv[k] = acc + Pm[L::C + k];
+    }
+  } else if constexpr (OK == PF_OBS_EXP_HALF) {
+    static_assert(NX == NZ, "EXP_HALF observes every component");
+    for (int q = t; q < NZ * NX; q += blockDim.x) {
+      const int k = q / NX, e = q - k * NX;
+      H[q] = (k == e) ? 0.5 * Pm[L::C + k] * exp(0.5 * eta[k]) : 0.0;
+    }
+    for (int k = t; k < NZ; k += blockDim.x) hv[k] = Pm[L::C + k] * exp(0.5 * eta[k]);
+  } else {  // ACOUSTIC: z_s = sum_c psi / (|p_c - s|^2 + d0)
+    static_assert(NX % 4 == 0, "acoustic state is 4 per target");
+    const double psi = Pm[L::AC], d0 = Pm[L::AC + 1];
+    for (int k = t; k < NZ; k += blockDim.x) {
+      const double sx = Pm[L::AC + 2 + k], sy = Pm[L::AC + 2 + NZ + k];
+      double acc = 0.0;
+      for (int c = 0; c < NX / 4; ++c) {
+        const double dx = eta[4 * c] - sx, dy = eta[4 * c + 1] - sy;
+        const double den = (dx * dx + dy * dy) + d0;
+        acc += psi / den;
+        const double den2 = den * den;
+        H[k * NX + 4 * c] = (-2.0 * psi * dx) / den2;
+        H[k * NX + 4 * c + 1] = (-2.0 * psi * dy) / den2;
+        H[k * NX + 4 * c + 2] = 0.0;
+        H[k * NX + 4 * c + 3] = 0.0;
+      }
+      hv[k] = acc;
+    }
+  }
+  __syncthreads();
+}
+
+// out = Gm (H v): zt scratch (NZ)
+template <int NX, int NZ>
+__device__ __forceinline__ void apply_A(const double* H, const double* Gm, const double* v, double* zt, double* out) {
+  const int t = threadIdx.x;
+  for (int k = t; k < NZ; k += blockDim.x) {
+    double acc = 0.0;
+    for (int e = 0; e < NX; ++e) acc += H[k * NX + e] * v[e];
+    zt[k] = acc;
+  }
+  __syncthreads();
+  for (int d = t; d < NX; d += blockDim.x) {
+    double acc = 0.0;
+    for (int l = 0; l < NZ; ++l) acc += Gm[d * NZ + l] * zt[l];
+    out[d] = acc;
+  }
+  __syncthreads();
+}
+
+// sum over the block of one value per thread (block = 64 lanes = one wave)
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int NX, int NZ, int TK, int OK>
+__global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
+  static_assert(NX <= 64 && NZ <= 64, "one lane per state / observation component");
+  using L = Lay<NX, NZ>;
+  using SM = WaveSmem<NX, NZ>;
+  __shared__ double sm[SM::SIZE];
+  const int t = threadIdx.x;
+  const double* __restrict__ Pm = p.Pm;
+  for (int q = t; q < NX * NX; q += 64) sm[SM::P + q] = p.Pk[q];
+  for (int q = t; q < NZ * NZ; q += 64) sm[SM::R + q] = Pm[L::R + q];
+  __syncthreads();
+  double* H = sm + SM::H;
+  double* K = sm + SM::K;
+  double* Mm = sm + SM::M;
+  double* aug = sm + SM::AUG;
+  double* Gm = sm + SM::GM;
+  double* eta = sm + SM::ET;
+  double* eta0 = sm + SM::E0;
+  double* t1 = sm + SM::T1;
+  double* t2 = sm + SM::T2;
+  double* cv = sm + SM::CV;
+  double* zt = sm + SM::ZT;
+  const double dlam = p.dlam;
+  for (int64_t i = blockIdx.x; i < p.N; i += gridDim.x) {
+    // ---- eta0 = g(x_{k-1}, u) + v -------------------------------------------
+    for (int d = t; d < NX; d += 64) sm[SM::XP + d] = p.x_in[(int64_t)d * p.Npad + i];
+    __syncthreads();
+    g_block<NX, NZ, TK>(sm + SM::XP, sm + SM::GX, t1, t2, Pm, p.u);
+    for (int d = t; d < NX; d += 64) {
+      double vd = 0.0;
+      if (p.noise == PF_NOISE_HOST) {
+        vd = p.v_host[i * NX + d];
+      } else if (p.noise == PF_NOISE_DEVICE) {
+        const int64_t f = i * NX + d;
+        t1[d] = normal4<double>(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS).v[f & 3];
+      }
+      sm[SM::V + d] = vd;
+    }
+    __syncthreads();
+    if (p.noise == PF_NOISE_DEVICE) {
+      for (int d = t; d < NX; d += 64) {
+        double acc = 0.0;
+        for (int e = 0; e <= d; ++e) acc += Pm[L::LQ + d * NX + e] * t1[e];
+        sm[SM::V + d] = acc;
+      }
+      __syncthreads();
+    }
+    for (int d = t; d < NX; d += 64) {
+      const double e0 = sm[SM::GX + d] + sm[SM::V + d];
+      eta0[d] = e0;
+      eta[d] = e0;
+    }
+    __syncthreads();
+    double theta = 0.0;
+    for (int j = 0; j < p.L; ++j) {
+      const double lam = p.lams[j];
+      // linearise at eta (ledh.py:143-145)
+      obs_jac_block<NX, NZ, OK>(eta, H, sm + SM::HV, Pm);
+      for (int k = t; k < NZ; k += 64) {
+        double acc = 0.0;
+        for (int e = 0; e < NX; ++e) acc += H[k * NX + e] * eta[e];
+        sm[SM::ZE + k] = sm[SM::HV + k] - acc;  // e = h(eta) - H eta
+      }
+      // K = P H^T
+      for (int q = t; q < NX * NZ; q += 64) {
+        const int d = q / NZ, k = q - d * NZ;
+        double acc = 0.0;
+        for (int e = 0; e < NX; ++e) acc += sm[SM::P + d * NX + e] * H[k * NX + e];
+        K[q] = acc;
+      }
+      __syncthreads();
+      // M = H K, S = lam M + R -> [S | I]; r = R^{-1}(z - e) into zt
+      for (int q = t; q < NZ * NZ; q += 64) {
+        const int k = q / NZ, l = q - k * NZ;
+        double acc = 0.0;
+        for (int d = 0; d < NX; ++d) acc += H[k * NX + d] * K[d * NZ + l];
+        Mm[q] = acc;
+        aug[k * 2 * NZ + l] = lam * acc + sm[SM::R + q];
+        aug[k * 2 * NZ + NZ + l] = (k == l) ? 1.0 : 0.0;
+      }
+      for (int k = t; k < NZ; k += 64) {
+        double acc = 0.0;
+        for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - sm[SM::ZE + l]);
+        zt[k] = acc;
+      }
+      __syncthreads();
+      if (i == 0 && p.diagS)
+        for (int q = t; q < NZ * NZ; q += 64) p.diagS[(int64_t)j * NZ * NZ + q] = aug[(q / NZ) * 2 * NZ + q % NZ];
+      // c = K r  (= P H^T R^{-1}(z - e))
+      for (int d = t; d < NX; d += 64) {
+        double acc = 0.0;
+        for (int k = 0; k < NZ; ++k) acc += K[d * NZ + k] * zt[k];
+        cv[d] = acc;
+      }
+      __syncthreads();
+      double S_ld;
+      int S_sg;
+      block_gauss_jordan(aug, NZ, sm + SM::FAC, &S_ld, &S_sg);
+      theta += flow_logdet<NX, NZ>(Mm, sm + SM::R, lam, dlam, S_ld, S_sg, sm + SM::TT, sm + SM::FAC);
+      // Gm = -1/2 K S^{-1}
+      for (int q = t; q < NX * NZ; q += 64) {
+        const int d = q / NZ, l = q - d * NZ;
+        double acc = 0.0;
+        for (int k = 0; k < NZ; ++k) acc += K[d * NZ + k] * aug[k * 2 * NZ + NZ + l];
+        Gm[q] = -0.5 * acc;
+      }
+      __syncthreads();
+      // b = (I + 2 lam A)[(I + lam A) c + A eta0]   (ledh.py:165)
+      apply_A<NX, NZ>(H, Gm, eta0, zt, t1);       // t1 = A eta0
+      apply_A<NX, NZ>(H, Gm, cv, zt, t2);         // t2 = A c
+      for (int d = t; d < NX; d += 64) t1[d] = (cv[d] + lam * t2[d]) + t1[d];  // w
+      __syncthreads();
+      apply_A<NX, NZ>(H, Gm, t1, zt, t2);         // t2 = A w
+      for (int d = t; d < NX; d += 64) t1[d] = t1[d] + 2.0 * lam * t2[d];      // b
+      __syncthreads();
+      apply_A<NX, NZ>(H, Gm, eta, zt, t2);        // t2 = A eta
+      for (int d = t; d < NX; d += 64) eta[d] = eta[d] + dlam * (t2[d] + t1[d]);  // ledh.py:171
+      __syncthreads();
+    }
+    // ---- weight (ledh.py:186-190) ---------------------------------------------
+    obs_jac_block<NX, NZ, OK>(eta, H, sm + SM::HV, Pm);
+    double part = 0.0;
+    for (int d = t; d < NX; d += 64) {  // (eta - gx)^T Q^{-1} (eta - gx) - v^T Q^{-1} v
+      double a = 0.0, b = 0.0;
+      for (int e = 0; e < NX; ++e) {
+        const double qi = Pm[L::QI + d * NX + e];
+        a += qi * (eta[e] - sm[SM::GX + e]);
+        b += qi * sm[SM::V + e];
+      }
+      part += (-0.5 * ((eta[d] - sm[SM::GX + d]) * a)) - (-0.5 * (sm[SM::V + d] * b));
+    }
+    for (int k = t; k < NZ; k += 64) {
+      double a = 0.0;
+      for (int l = 0; l < NZ; ++l) a += Pm[L::RI + k * NZ + l] * (p.z[l] - sm[SM::HV + l]);
+      part += -0.5 * ((p.z[k] - sm[SM::HV + k]) * a);
+    }
+    const double tot = wave_sum64(part);
+    if (t == 0) p.lw[i] = (log(p.w_in[i] + 1e-300) + theta) + tot;
+    for (int d = t; d < NX; d += 64) p.x_out[(int64_t)d * p.Npad + i] = eta[d];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight pipeline
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double block_reduce_sum(double v, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum64(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += red[k];
+  __syncthreads();
+  return s;
+}
+__device__ __forceinline__ double block_reduce_max(double v, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = red[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) s = fmax(s, red[k]);
+  __syncthreads();
+  return s;
+}
+
+struct WParams {
+  double* x_in;        // [NX][Npad] current particles
+  double* x_out;       // [NX][Npad] resample target
+  const double* lw;    // [N]
+  double* w;           // [N] weights (normalised in place)
+  double* w_out;       // [N] resample target weights
+  double* tmax;        // [G]
+  double* tsum;        // [G]
+  double* trec;        // [G][2 + NX]  sum w, sum w^2, sum w x (per tile)
+  double* cdf;         // [N]
+  double* stat;        // [8]: ess, flag, sw, ...
+  double* mean;        // [NX]
+  double* cpart;       // [Gc][NX(NX+1)/2]
+  double* o_mean;      // output mean [NX] (nullable)
+  double* o_cov;       // output cov [NX][NX] (nullable)
+  double* o_ess;       // output ess (nullable)
+  int32_t* o_flag;     // output flag (nullable)
+  const double* unif;  // host U [1] or null
+  int64_t N, Npad;
+  int G, Gc;
+  double ratio;
+  uint64_t seed;
+  uint32_t epoch;
+  int uniform;         // weights are exactly 1/N (after init / resample)
+};
+
+// tile max of the log weights
+__global__ void __launch_bounds__(TB) k_tile_max(WParams p) {
+  __shared__ double red[TB / 64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
+  double m = -INFINITY;
+  for (int64_t i = o0 + t; i < o1; i += TB) m = fmax(m, p.lw[i]);
+  m = block_reduce_max(m, red);
+  if (t == 0) p.tmax[b] = m;
+}
+
+// global max (every workgroup, same order), e_i = exp(l_i - max), tile sums
+__global__ void __launch_bounds__(TB) k_exp_sum(WParams p) {
+  __shared__ double red[TB / 64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  double m = -INFINITY;
+  for (int k = t; k < p.G; k += TB) m = fmax(m, p.tmax[k]);
+  m = block_reduce_max(m, red);
+  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
+  double s = 0.0;
+  for (int64_t i = o0 + t; i < o1; i += TB) {
+    const double e = exp(p.lw[i] - m);
+    p.w[i] = e;
+    s += e;
+  }
+  s = block_reduce_sum(s, red);
+  if (t == 0) p.tsum[b] = s;
+}
+
+// w /= sum(w) (ledh.py:195); per tile: sum w, sum w^2  (trec width 2)
+__global__ void __launch_bounds__(TB) k_normalise(WParams p) {
+  __shared__ double red[TB / 64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  double S = 0.0;
+  for (int k = t; k < p.G; k += TB) S += p.tsum[k];
+  S = block_reduce_sum(S, red);
+  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t i = o0 + t; i < o1; i += TB) {
+    const double wi = p.w[i] / S;
+    p.w[i] = wi;
+    a0 += wi;
+    a1 += wi * wi;
+  }
+  a0 = block_reduce_sum(a0, red);
+  a1 = block_reduce_sum(a1, red);
+  if (t == 0) {
+    p.trec[(int64_t)b * 2] = a0;
+    p.trec[(int64_t)b * 2 + 1] = a1;
+  }
+}
+
+// ESS of the normalised weights (ledh.py:39-41, 202) and the resample decision (:201-203)
+__global__ void __launch_bounds__(TB) k_decide(WParams p, int rec_w) {
+  __shared__ double red[TB / 64];
+  const int t = threadIdx.x;
+  double sw = 0.0, sw2 = 0.0;
+  for (int k = t; k < p.G; k += TB) {
+    sw += p.trec[(int64_t)k * rec_w];
+    sw2 += p.trec[(int64_t)k * rec_w + 1];
+  }
+  sw = block_reduce_sum(sw, red);
+  sw2 = block_reduce_sum(sw2, red);
+  if (t == 0) {
+    const double ess = 1.0 / (sw2 / (sw * sw));
+    const int flag = (p.ratio > 0.0) && (ess < p.ratio * (double)p.N);
+    p.stat[0] = ess;
+    p.stat[1] = flag;
+    p.stat[2] = sw;
+    if (p.o_ess) *p.o_ess = ess;
+    if (p.o_flag) *p.o_flag = flag;
+  }
+}
+
+// systematic resampling CDF: cdf_i = (prefix of tile sums + in-tile inclusive scan) / sum(w)
+__global__ void __launch_bounds__(TB) k_cdf(WParams p, int rec_w) {
+  __shared__ double red[TB / 64];
+  __shared__ double sc[TB];
+  if (p.stat[1] == 0.0) return;
+  const int b = blockIdx.x, t = threadIdx.x;
+  double pre = 0.0;
+  for (int k = t; k < b; k += TB) pre += p.trec[(int64_t)k * rec_w];
+  pre = block_reduce_sum(pre, red);
+  const double sw = p.stat[2];
+  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
+  constexpr int PER = LT / TB;
+  const int64_t s0 = o0 + (int64_t)t * PER;
+  double loc[PER];
+  double run = 0.0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int64_t i = s0 + q;
+    run += (i < o1) ? p.w[i] : 0.0;
+    loc[q] = run;
+  }
+  sc[t] = run;
+  __syncthreads();
+  double off = 0.0;
+  for (int k = 0; k < t; ++k) off += sc[k];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int64_t i = s0 + q;
+    if (i < o1) p.cdf[i] = (pre + (off + loc[q])) / sw;
+  }
+}
+
+// ancestors: idx_i = first j with (U + i)/N < cdf_j (ledh.py:28-37), clamped; gather x, w = 1/N
+template <int NX>
+__global__ void __launch_bounds__(TB) k_gather(WParams p) {
+  if (p.stat[1] == 0.0) return;
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (i >= p.N) return;
+  const double U = p.unif ? p.unif[0] : uniform53(p.seed, 0u, 0u, p.epoch);
+  const double pos = (U + (double)i) / (double)p.N;
+  int64_t lo = 0, hi = p.N;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (pos < p.cdf[mid]) hi = mid; else lo = mid + 1;
+  }
+  const int64_t a = lo < p.N ? lo : p.N - 1;
+#pragma unroll
+  for (int d = 0; d < NX; ++d) p.x_out[(int64_t)d * p.Npad + i] = p.x_in[(int64_t)d * p.Npad + a];
+  p.w_out[i] = 1.0 / (double)p.N;
+}
+
+// after a device-decided resample: copy the gathered set back (x_out -> x_in, w_out -> w)
+template <int NX>
+__global__ void __launch_bounds__(TB) k_commit(WParams p) {
+  if (p.stat[1] == 0.0) return;
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (i >= p.N) return;
+#pragma unroll
+  for (int d = 0; d < NX; ++d) p.x_in[(int64_t)d * p.Npad + i] = p.x_out[(int64_t)d * p.Npad + i];
+  p.w[i] = p.w_out[i];
+}
+
+// weighted mean, part 1: per tile sum w, sum w x  (ledh.py:217-220)
+template <int NX>
+__global__ void __launch_bounds__(TB) k_mean_part(WParams p) {
+  __shared__ double red[TB / 64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
+  double a[1 + NX];
+#pragma unroll
+  for (int q = 0; q < 1 + NX; ++q) a[q] = 0.0;
+  for (int64_t i = o0 + t; i < o1; i += TB) {
+    const double wi = p.uniform ? 1.0 / (double)p.N : p.w[i];
+    a[0] += wi;
+#pragma unroll
+    for (int d = 0; d < NX; ++d) a[1 + d] += p.x_in[(int64_t)d * p.Npad + i] * wi;
+  }
+#pragma unroll
+  for (int q = 0; q < 1 + NX; ++q) {
+    const double s = block_reduce_sum(a[q], red);
+    if (t == 0) p.trec[(int64_t)b * (1 + NX) + q] = s;
+  }
+}
+
+template <int NX>
+__global__ void __launch_bounds__(TB) k_mean(WParams p) {
+  __shared__ double red[TB / 64];
+  const int t = threadIdx.x;
+  double sw = 0.0;
+  for (int k = t; k < p.G; k += TB) sw += p.trec[(int64_t)k * (1 + NX)];
+  sw = block_reduce_sum(sw, red);
+  for (int d = 0; d < NX; ++d) {
+    double s = 0.0;
+    for (int k = t; k < p.G; k += TB) s += p.trec[(int64_t)k * (1 + NX) + 1 + d];
+    s = block_reduce_sum(s, red);
+    if (t == 0) {
+      p.mean[d] = s / sw;
+      if (p.o_mean) p.o_mean[d] = s / sw;
+    }
+  }
+  if (t == 0) p.stat[3] = sw;
+}
+
+// weighted covariance, part 1: per tile of CT particles, sum w (x-m)(x-m)^T (upper triangle)
+template <int NX>
+__global__ void __launch_bounds__(TB) k_cov_part(WParams p) {
+  constexpr int NP = NX * (NX + 1) / 2;
+  __shared__ double xs[CT * NX];
+  __shared__ double ws[CT];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int64_t o0 = (int64_t)b * CT;
+  const int n = (int)min((int64_t)CT, p.N - o0);
+  for (int q = t; q < CT * NX; q += TB) {
+    const int j = q / NX, d = q - j * NX;
+    xs[q] = j < n ? p.x_in[(int64_t)d * p.Npad + o0 + j] - p.mean[d] : 0.0;
+  }
+  for (int j = t; j < CT; j += TB) ws[j] = j < n ? (p.uniform ? 1.0 / (double)p.N : p.w[o0 + j]) : 0.0;
+  __syncthreads();
+  for (int q = t; q < NP; q += TB) {
+    // q -> (d, e) with d <= e, row-major upper triangle
+    int d = 0, rem = q;
+    while (rem >= NX - d) { rem -= NX - d; ++d; }
+    const int e = d + rem;
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j) acc += (xs[j * NX + d] * ws[j]) * xs[j * NX + e];
+    p.cpart[(int64_t)b * NP + q] = acc;
+  }
+}
+
+template <int NX>
+__global__ void __launch_bounds__(TB) k_cov(WParams p) {
+  constexpr int NP = NX * (NX + 1) / 2;
+  const int t = threadIdx.x;
+  const double sw = p.stat[3];
+  for (int q = t; q < NP; q += TB) {
+    int d = 0, rem = q;
+    while (rem >= NX - d) { rem -= NX - d; ++d; }
+    const int e = d + rem;
+    double acc = 0.0;
+    for (int k = 0; k < p.Gc; ++k) acc += p.cpart[(int64_t)k * NP + q];
+    const double c = acc / sw;
+    if (p.o_cov) {
+      p.o_cov[d * NX + e] = c;
+      p.o_cov[e * NX + d] = c;
+    }
+  }
+}
+
+// initial particles: x = mean0 + eps, eps = host draw [N][NX] or chol(cov0) n (Philox)
+template <int NX>
+__global__ void __launch_bounds__(TB) k_init(double* x, double* w, const double* mean0, const double* Lc,
+                                              const double* eps, int64_t N, int64_t Npad, uint64_t seed,
+                                              uint32_t epoch) {
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (i >= N) return;
+  double n[NX];
+  if (!eps) {
+#pragma unroll
+    for (int d = 0; d < NX; ++d) {
+      const int64_t f = i * NX + d;
+      n[d] = normal4<double>(seed, (uint32_t)(f >> 2), 0u, epoch, STREAM_INIT).v[f & 3];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < NX; ++d) {
+    double e;
+    if (eps) {
+      e = eps[i * NX + d];
+    } else {
+      e = 0.0;
+#pragma unroll
+      for (int c = 0; c <= d; ++c) e += Lc[d * NX + c] * n[c];
+    }
+    x[(int64_t)d * Npad + i] = mean0[d] + e;
+  }
+  w[i] = 1.0 / (double)N;
+}
+
+}  // namespace ledh
+}  // namespace pf

@@ -77,9 +77,10 @@ class LinearTransition(Transition):
     def params(self):
         return np.ascontiguousarray(self.A.ravel())
 
-    def __call__(self, x, u=None):
+    def __call__(self, x, u=None, v=None):
         x = np.asarray(x, float)
-        return self.A @ x if u is None else self.A @ x + u
+        y = self.A @ x if u is None else self.A @ x + u
+        return y if v is None else y + v
 
 
 class SVTransition(LinearTransition):
@@ -89,10 +90,11 @@ class SVTransition(LinearTransition):
         self.alpha = np.atleast_1d(np.asarray(alpha, float))
         super().__init__(np.diag(self.alpha))
 
-    def __call__(self, x, u=None):
+    def __call__(self, x, u=None, v=None):
         x = np.atleast_1d(np.asarray(x, float))
         y = self.alpha * x
-        return y if u is None else y + u
+        y = y if u is None else y + u
+        return y if v is None else y + v
 
 
 class CVTransition(LinearTransition):
@@ -107,12 +109,13 @@ class CVTransition(LinearTransition):
         self.F = F
         super().__init__(np.kron(np.eye(n_targets), F))
 
-    def __call__(self, x, u=None):
+    def __call__(self, x, u=None, v=None):
         x = np.asarray(x, float)
         out = np.zeros(4 * self.n_targets)
         for c in range(self.n_targets):
             out[4 * c:4 * c + 4] = self.F @ x[4 * c:4 * c + 4]
-        return out if u is None else out + u
+        out = out if u is None else out + u
+        return out if v is None else out + v
 
 
 class L96Transition(Transition):
@@ -131,7 +134,7 @@ class L96Transition(Transition):
     def _rhs(self, x):
         return (np.roll(x, -1) - np.roll(x, 2)) * np.roll(x, 1) - x + self.F
 
-    def __call__(self, x, u=None):
+    def __call__(self, x, u=None, v=None):
         x = np.asarray(x, float)
         dt = self.dt
         k1 = self._rhs(x)
@@ -139,7 +142,34 @@ class L96Transition(Transition):
         k3 = self._rhs(x + 0.5 * dt * k2)
         k4 = self._rhs(x + dt * k3)
         y = x + (dt / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
-        return y if u is None else y + u
+        y = y if u is None else y + u
+        return y if v is None else y + v
+
+    def jacobian(self, x, u=None):
+        """Tangent-linear map of one RK4 step at x (analytic EKF Jacobian of g)."""
+        x = np.asarray(x, float)
+        n, dt, F = self.nx, self.dt, self.F
+        idx = np.arange(n)
+
+        def J_rhs(y):  # d/dy of (y[a+1] - y[a-2]) y[a-1] - y[a] + F
+            J = -np.eye(n)
+            J[idx, (idx + 1) % n] += y[(idx - 1) % n]
+            J[idx, (idx - 2) % n] -= y[(idx - 1) % n]
+            J[idx, (idx - 1) % n] += y[(idx + 1) % n] - y[(idx - 2) % n]
+            return J
+
+        I = np.eye(n)
+        k1 = self._rhs(x)
+        y2 = x + 0.5 * dt * k1
+        k2 = self._rhs(y2)
+        y3 = x + 0.5 * dt * k2
+        k3 = self._rhs(y3)
+        y4 = x + dt * k3
+        D1 = J_rhs(x)
+        D2 = J_rhs(y2) @ (I + 0.5 * dt * D1)
+        D3 = J_rhs(y3) @ (I + 0.5 * dt * D2)
+        D4 = J_rhs(y4) @ (I + dt * D3)
+        return I + (dt / 6.0) * (D1 + 2 * D2 + 2 * D3 + D4)
 
 
 # ---------------------------------------------------------------------------
@@ -160,6 +190,9 @@ class LinearObservation(Observation):
 
     def __call__(self, x):
         return self.H @ np.asarray(x, float) + self.c
+
+    def jacobian(self, x):
+        return self.H.copy()
 
 
 class SVLogSqObservation(LinearObservation):
@@ -205,6 +238,10 @@ class ExpHalfObservation(Observation):
         x = np.atleast_1d(np.asarray(x, float))
         return self.beta * np.exp(0.5 * x)
 
+    def jacobian(self, x):
+        x = np.atleast_1d(np.asarray(x, float))
+        return np.diag(0.5 * self.beta * np.exp(0.5 * x))
+
 
 class AcousticObservation(Observation):
     """Summed acoustic amplitudes ``z_s = sum_c psi / (|p_c - s|^2 + d0)`` of
@@ -234,6 +271,50 @@ class AcousticObservation(Observation):
                 zc[s] = self.psi / (np.sum((pos - self.S[s]) ** 2) + self.d0)
             z += zc
         return z
+
+    def jacobian(self, x):
+        """Analytic dh/dx (test_filters_mat_simulator.py:55-64, summed over targets)."""
+        x = np.asarray(x, float)
+        H = np.zeros((self.nz, self.nx))
+        for c in range(self.n_targets):
+            pos = x[4 * c:4 * c + 2]
+            for s in range(self.nz):
+                diff = pos - self.S[s]
+                denom = (np.sum(diff ** 2) + self.d0) ** 2
+                H[s, 4 * c] = -2.0 * self.psi * diff[0] / denom
+                H[s, 4 * c + 1] = -2.0 * self.psi * diff[1] / denom
+        return H
+
+
+# ---------------------------------------------------------------------------
+# Gaussian log densities of the LEDH weight (ledh.py:21-22 LogTransPdf / LogLikePdf)
+# ---------------------------------------------------------------------------
+class GaussianTransitionDensity:
+    """``log p(x_k | x_{k-1}) = log N(x_k; g(x_{k-1}), Q)`` — the transition density of every
+    LEDH wiring in the reference tests (test_ledh_flow_pf.py:92-95,
+    test_filters_mat_simulator.py:66-70).  Callable with the reference's signature; the
+    engine evaluates it on the device from (g, Q)."""
+
+    def __init__(self, g: Transition, Q):
+        self.g = g
+        self.Q = np.atleast_2d(np.asarray(Q, float))
+
+    def __call__(self, xk, xkm1):
+        diff = np.atleast_1d(np.asarray(xk, float)) - self.g(xkm1)
+        return -0.5 * (diff.T @ np.linalg.solve(self.Q, diff) + np.log(np.linalg.det(2 * np.pi * self.Q)))
+
+
+class GaussianLikelihood:
+    """``log p(z | x) = log N(z; h(x), R)`` (test_ledh_flow_pf.py:97-100,
+    test_filters_mat_simulator.py:72-77)."""
+
+    def __init__(self, h: Observation, R):
+        self.h = h
+        self.R = np.atleast_2d(np.asarray(R, float))
+
+    def __call__(self, z, x):
+        diff = np.atleast_1d(np.asarray(z, float)) - self.h(x)
+        return -0.5 * (diff.T @ np.linalg.solve(self.R, diff) + np.log(np.linalg.det(2 * np.pi * self.R)))
 
 
 def is_device_model(g, h) -> bool:

@@ -19,28 +19,31 @@ from particle_filters_amd import _native as NV
 from particle_filters_amd import models as M
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "pf_engine.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("pf_engine.h", "pf_ledh.h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(pf_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    names = []
+    for hdr in HEADERS:
+        src = open(hdr).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(pf_[a-z_0-9]+)\s*\(", src, flags=re.M)
     return sorted(set(names))
 
 
 def test_header_parses_all_entry_points():
     names = header_functions()
-    assert len(names) >= 20
+    assert len(names) >= 30
     for must in ("pf_create", "pf_destroy", "pf_initialize", "pf_predict", "pf_update", "pf_resample",
-                 "pf_run", "pf_run_device", "pf_resample_indices", "pf_last_error"):
+                 "pf_run", "pf_run_device", "pf_resample_indices", "pf_last_error",
+                 "pf_ledh_create", "pf_ledh_init", "pf_ledh_step", "pf_ledh_finish", "pf_ledh_run"):
         assert must in names
 
 
 def test_library_exports_every_declared_symbol():
     lib = C.CDLL(NV.LIB_PATH)
     missing = [n for n in header_functions() if not hasattr(lib, n)]
-    assert not missing, f"declared in pf_engine.h but not exported: {missing}"
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
 
 
 def test_binding_covers_header_exactly():
@@ -122,3 +125,18 @@ def test_describe_validates_shapes():
         M.describe(M.SVTransition(0.95), M.SVLogSqObservation(1.0), np.eye(2), np.eye(1))
     with pytest.raises(ValueError):
         M.describe(M.SVTransition(0.95), M.SVLogSqObservation(1.0), np.eye(1), np.eye(2))
+
+
+def test_ledh_model_registry_and_validation():
+    lib = NV.load()
+    assert lib.pf_ledh_model_supported(40, 10, NV.PF_TRANS_L96, NV.PF_OBS_LINEAR)
+    assert lib.pf_ledh_model_supported(1, 1, NV.PF_TRANS_LINEAR, NV.PF_OBS_EXP_HALF)
+    assert lib.pf_ledh_model_supported(4, 9, NV.PF_TRANS_LINEAR, NV.PF_OBS_ACOUSTIC)
+    assert not lib.pf_ledh_model_supported(7, 3, NV.PF_TRANS_L96, NV.PF_OBS_ACOUSTIC)
+    d, keep = M.describe(M.SVTransition(0.9), M.LinearObservation([[1.0]]), np.eye(1) * 0.04, np.eye(1) * 0.1)
+    h_ = C.c_void_p()
+    opts = NV.LedhOpts(0, 8, 0.5, 1, 0, 0)
+    assert lib.pf_ledh_create(C.byref(d), C.byref(opts), C.byref(h_)) == NV.PF_E_ARG and not h_.value
+    d2, keep2 = M.describe(M.LinearTransition(np.eye(5)), M.LinearObservation(np.ones((1, 5))), np.eye(5), np.eye(1))
+    opts = NV.LedhOpts(10, 8, 0.5, 1, 0, 0)
+    assert lib.pf_ledh_create(C.byref(d2), C.byref(opts), C.byref(h_)) == NV.PF_E_UNSUPPORTED

@@ -1,0 +1,161 @@
+"""HIP LEDH flow filter vs the reference's own outputs and the oracle (-m gpu, MI355X).
+
+tests/golden/ledh_runs.npz holds the reference LEDHFlowPF + EKF run on fixed seeds
+(tests/golden/make_golden_ledh.py).  The engine in rng_mode="host" consumes the
+identical random stream (initial multivariate_normal, the process_noise_sampler's
+draws, the resampling uniform), so its outputs are compared per step.
+
+Tolerances (fp64 engine): the flow is evaluated in observation space (matrix
+determinant lemma, A v = Gm (H v); see pf_ledh_kernels.h) and reductions run in a
+different order, so agreement is to rounding amplified by the flow: posterior
+means within 1e-9 (relative to the state scale), covariances within 1e-8,
+condition-number diagnostics within rtol 1e-6; resample decisions identical.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from particle_filters_amd import ledh as LD
+from particle_filters_amd import models as M
+from particle_filters_amd import trackers as TR
+from oracle import ledh_oracle as LO
+
+pytestmark = pytest.mark.gpu
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ledh_runs.npz"))
+MAT = np.load(os.path.join(os.path.dirname(__file__), "golden", "mat_data.npz"))
+L96 = np.load(os.path.join(os.path.dirname(__file__), "golden", "l96_data.npz"))
+NAMES = [str(n) for n in GOLD["names"]]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    from particle_filters_amd import _native
+    assert _native.device_count() > 0, "no HIP device visible: -m gpu tests must run on an MI355X"
+
+
+def case(name):
+    g = {k.split("__", 1)[1]: GOLD[k] for k in GOLD.files if k.startswith(name + "__")}
+    psi, d0 = float(MAT["meta2"][2]), float(MAT["meta2"][3])
+    if name.startswith("lin1d"):
+        om = LO.linear_1d()
+        gm, hm = M.SVTransition(0.9), M.LinearObservation([[1.0]])
+    elif name == "sv_exp":
+        om = LO.sv_exp_half(0.95, 0.2, 1.0, 0.1)
+        gm, hm = M.SVTransition(0.95), M.ExpHalfObservation(1.0)
+    elif name == "acoustic":
+        om = LO.acoustic_single(MAT["S2"], psi=psi, d0=d0)
+        gm, hm = M.CVTransition(1, 1.0), M.AcousticObservation(MAT["S2"], psi, d0, 1)
+    elif name == "l96":
+        om = LO.lorenz96(40)
+        gm, hm = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+    else:
+        raise KeyError(name)
+    return om, gm, hm, g
+
+
+def make_filter(name, flow="auto", rng_mode="host", n_particles=None, ratio=None, seed=None):
+    om, gm, hm, g = case(name)
+    ekf = TR.ExtendedKalmanFilter(om.g_ekf, om.h, om.Q, om.R, jac_g=om.jac_g, jac_h=om.jac_h)
+    tracker = TR.EKFTracker(ekf, TR.EKFState(np.asarray(g["mean0"], float).copy(),
+                                             np.asarray(g["cov0"], float).copy(), 0))
+    cfg = LD.LEDHConfig(n_particles=int(g["n_particles"]) if n_particles is None else n_particles,
+                        n_lambda_steps=int(g["n_lambda"]),
+                        resample_ess_ratio=float(g["ratio"]) if ratio is None else ratio,
+                        rng=np.random.default_rng(int(g["seed"]) if seed is None else seed))
+    pf = LD.LEDHFlowPF(tracker, gm, hm, hm.jacobian, M.GaussianTransitionDensity(gm, om.Q),
+                       M.GaussianLikelihood(hm, om.R), om.R, cfg, rng_mode=rng_mode, flow=flow)
+    return pf, cfg, om, g
+
+
+@pytest.mark.parametrize("flow", ["auto", "per_particle"])
+@pytest.mark.parametrize("name", NAMES)
+def test_step_matches_reference(name, flow):
+    pf, cfg, om, g = make_filter(name, flow=flow)
+    if flow == "auto":
+        assert pf.shared_jacobian_path == (name in ("lin1d", "lin1d_nonoise", "l96"))
+    st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+    np.testing.assert_array_equal(st.particles, g["init_particles"])
+    np.testing.assert_allclose(st.mean, g["init_mean"], rtol=0, atol=1e-12 * max(1.0, np.abs(g["init_mean"]).max()))
+    np.testing.assert_allclose(st.cov, g["init_cov"], rtol=1e-10, atol=1e-12)
+    noise = bool(g["noise"]) if "noise" in g else True
+    sampler = (lambda n, nx: cfg.rng.multivariate_normal(np.zeros(nx), om.Q, size=n)) if noise else None
+    scale = max(1.0, float(np.abs(g["means"]).max()))
+    for t in range(len(g["Z"])):
+        st = pf.step(st, g["Z"][t], process_noise_sampler=sampler)
+        assert pf.last_resampled == bool(g["flags"][t]), f"resample decision differs at step {t}"
+        np.testing.assert_allclose(st.mean, g["means"][t], rtol=0, atol=1e-9 * scale, err_msg=f"mean t={t}")
+        cs = max(1.0, float(np.abs(g["covs"][t]).max()))
+        np.testing.assert_allclose(st.cov, g["covs"][t], rtol=0, atol=1e-8 * cs, err_msg=f"cov t={t}")
+        np.testing.assert_allclose(st.weights, g["weights"][t], rtol=1e-7, atol=1e-13, err_msg=f"w t={t}")
+        np.testing.assert_allclose(st.particles, g["particles"][t], rtol=0, atol=1e-9 * scale, err_msg=f"x t={t}")
+        np.testing.assert_allclose(st.diagnostics["condition_numbers"], g["conds"][t], rtol=1e-6)
+
+
+def test_run_equals_step_without_noise():
+    """pf_ledh_run (device-resident loop, tracker covariances uploaded up front) reproduces
+    the step API when nothing random happens after the initial draw (no process noise,
+    no resampling)."""
+    name = "l96"
+    pf1, cfg1, om, g = make_filter(name, ratio=0.0)
+    st1 = pf1.init_from_gaussian(g["mean0"], g["cov0"])
+    means = []
+    for t in range(len(g["Z"])):
+        st1 = pf1.step(st1, g["Z"][t])
+        means.append(st1.mean)
+    pf2, _, _, _ = make_filter(name, ratio=0.0)
+    st2 = pf2.init_from_gaussian(g["mean0"], g["cov0"])
+    res = pf2.run(st2, g["Z"], process_noise="none")
+    np.testing.assert_allclose(res.means, np.array(means), rtol=0, atol=1e-12 * 10)
+    np.testing.assert_allclose(pf2.state.particles, st1.particles, rtol=0, atol=1e-11)
+    assert not res.flags.any()
+
+
+def truth(name, T):
+    if name == "l96":
+        return L96["truth"][1:T + 1]
+    if name == "acoustic":
+        return MAT["X2"][1:T + 1, 0]
+    sv = np.load(os.path.join(os.path.dirname(__file__), "golden", "sv_data.npz"))
+    return sv["X0"][1:T + 1, None]
+
+
+@pytest.mark.parametrize("name", ["l96", "acoustic", "sv_exp"])
+def test_device_rng_run_statistics(name):
+    """Device noise + device resampling (Philox) vs the oracle with NumPy noise: the
+    RMSE of the posterior means against the simulator's truth agrees (independent
+    Monte-Carlo draws, so within a band, not to rounding)."""
+    om, gm, hm, g = case(name)
+    n = 2000
+    pf, cfg, _, _ = make_filter(name, rng_mode="device", n_particles=n, seed=11)
+    st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+    res = pf.run(st, g["Z"], process_noise="device")
+    assert np.all(np.isfinite(res.means)) and np.all(np.isfinite(res.covs))
+    assert np.all(res.ess > 0) and np.all(res.ess <= n * (1 + 1e-9))
+    tr = truth(name, len(g["Z"]))
+    rm_e = res.rmse(tr)
+    rm_o = []
+    for seed in (11, 12, 13):
+        o = LO.run_ledh(om, g["Z"], mean0=g["mean0"], cov0=g["cov0"], n_particles=n,
+                        n_lambda_steps=int(g["n_lambda"]), ratio=float(g["ratio"]), seed=seed, vectorized=True)
+        rm_o.append(float(np.sqrt(np.mean((o["means"] - tr.reshape(o["means"].shape)) ** 2))))
+    lo, hi = min(rm_o), max(rm_o)
+    assert 0.5 * lo - 0.05 <= rm_e <= 1.5 * hi + 0.05, (rm_e, rm_o)
+
+
+def test_large_l96_shared_vs_per_particle():
+    """The shared-Jacobian flow and the per-particle flow agree for a linear h at N = 4096."""
+    name = "l96"
+    out = {}
+    for flow in ("auto", "per_particle"):
+        pf, cfg, om, g = make_filter(name, flow=flow, n_particles=4096, seed=5)
+        st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+        sampler = lambda n, nx: cfg.rng.multivariate_normal(np.zeros(nx), om.Q, size=n)  # noqa: E731
+        ms = []
+        for t in range(len(g["Z"])):
+            st = pf.step(st, g["Z"][t], process_noise_sampler=sampler)
+            ms.append(st.mean)
+        out[flow] = np.array(ms)
+    np.testing.assert_allclose(out["auto"], out["per_particle"], rtol=0, atol=1e-8)
