@@ -18,6 +18,7 @@ Workloads (BASELINE.json configs; the default is the headline metric's config):
   l96  config 3: Lorenz-96 d = 40 (RK4 g, every 4th component observed), N = 1e5
   mat  config 4: joint 4-target acoustic tracking (nx = 16, nz = 25), N = 1e5,
        8 replicates per GPU (64 over 8 GPUs)
+  ledh config 5: LEDH particle flow on L96 d = 40, N = 1e4, 8 lambda steps (fp64)
 
 Extra JSON fields:
   roofline      dominant kernel.  SV: k_resident<f32, SV> — ONE launch runs all K
@@ -171,7 +172,123 @@ class MAT(Workload):
                 "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
 
 
-WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT}
+WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT, "ledh": None}
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector 157.3 TF of MI355X_MICROARCH.md)
+
+
+def ledh_flops_per_particle(nx, nz, L):
+    """Algorithmic FP64 flops of one particle-step of the shared-Jacobian LEDH flow
+    (pf_ledh_kernels.h k_flow_shared): RK4 g (4 rhs x 4 nx + 3 stage axpys x 2 nx + final
+    3 nx), chol(Q) noise (nx(nx+1)/2 FMA), y0 = H eta0 (nx nz FMA), per lambda step
+    2 nz^2 + nx nz FMA + ~4 nz + 3 nx, two diagonal quadratic forms (2 nx) + one nz^2."""
+    rk4 = 4 * 4 * nx + 3 * 2 * nx * 2 + 3 * nx
+    noise = nx * (nx + 1)  # FMA = 2 flops
+    y0 = 2 * nx * nz
+    per_lam = 2 * (2 * nz * nz + nx * nz) + 4 * nz + 3 * nx
+    quad = 2 * 2 * nx + 2 * nz * nz
+    return rk4 + noise + y0 + L * per_lam + quad
+
+
+def main_ledh(args, world, rank, local):
+    """BASELINE config 5: LEDH particle flow on Lorenz-96 d = 40, N = 1e4, 8 lambda steps."""
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from particle_filters_amd import ledh as LD, models as M, simulators as S, trackers as TR
+
+    K = args.steps if args.steps is not None else 200
+    W = args.warmup if args.warmup is not None else 20
+    Np, L, nx, nz = 10_000, 8, 40, 10
+    sim = S.simulate_lorenz96(nx=40, F=8.0, dt=0.01, spinup_steps=1000, total_steps=W + K, Np=1, obs_interval=1,
+                              obs_fraction=4, obs_error_std=1.0, seed=42)
+    g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(sim.H_idx, 40)
+    Q, R = 0.1 ** 2 * np.eye(40), sim.R
+    mean0, cov0 = sim.ensemble_traj[0, 0], 2.0 * np.eye(40)
+
+    def make():
+        ekf = TR.ExtendedKalmanFilter(g, h, Q, R, jac_g=g.jacobian, jac_h=h.jacobian)
+        tracker = TR.EKFTracker(ekf, TR.EKFState(mean0.copy(), cov0.copy(), 0))
+        cfg = LD.LEDHConfig(n_particles=Np, n_lambda_steps=L, resample_ess_ratio=0.5,
+                            rng=np.random.default_rng(42 + rank))
+        pf = LD.LEDHFlowPF(tracker, g, h, h.jacobian, M.GaussianTransitionDensity(g, Q), M.GaussianLikelihood(h, R), R,
+                           cfg, rng_mode="device")
+        return pf, tracker
+
+    Z = sim.observations[1:]
+    pf, tracker = make()
+    st = pf.init_from_gaussian(mean0, cov0)
+    pf.run(st, Z[:max(W, 1)])  # warm-up (same sequence as the timed run)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    Ps = np.empty((K, nx, nx))
+    for t in range(K):  # the host tracker (never sees particles): run ahead over Z
+        _, P = tracker.predict()
+        Ps[t] = P
+        tracker.update(Z[W + t])
+    t_tr = time.perf_counter() - t0
+    res = pf.run(pf.state, Z[W:W + K], tracker_covs=Ps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    dev_s = elapsed - t_tr
+    rmse = res.rmse(sim.truth_traj[W + 1:W + K + 1])
+    flops = ledh_flops_per_particle(nx, nz, L) * Np * K
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import ledh_oracle as LO
+
+            om = LO.lorenz96(40)
+            steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", "1"))
+            n_cpu = 1000
+            tr = LO.make_ekf_tracker(om, mean0, cov0)
+            opf = LO.LEDHOracle(tr, om, n_particles=n_cpu, n_lambda_steps=L, resample_ess_ratio=0.5,
+                                rng=np.random.default_rng(1), vectorized=False)
+            ost = opf.init_from_gaussian(mean0, cov0)
+            sampler = lambda n, d: opf.rng.multivariate_normal(np.zeros(d), om.Q, size=n)  # noqa: E731
+            c0 = time.perf_counter()
+            for t in range(steps):
+                ost = opf.step(ost, Z[t], process_noise_sampler=sampler)
+            cdt = time.perf_counter() - c0
+            cpu = {"value": n_cpu * steps / cdt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                   "sample": f"LEDH L96 d=40, N={n_cpu}, L={L}, {steps} step(s), faithful per-particle restatement "
+                             f"(oracle/ledh_oracle.py, bit-identical to the reference LEDHFlowPF), {cdt:.1f} s",
+                   "cores_on_host": os.cpu_count()}
+        line = {
+            "metric": "particle-steps/sec (N×T/s), LEDH flow filter L96 d=40",
+            "value": Np * K * world / elapsed, "unit": "particle-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": elapsed * 1e3 / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)",
+            "config": {"workload": "LEDH particle-flow PF (BASELINE config 5): L96 d=40, N=1e4 particles, 8 lambda "
+                                   "steps, ESS-ratio 0.5 systematic resampling, EKF tracker (host, analytic RK4 "
+                                   "Jacobian), Philox process noise",
+                       "n_particles": Np, "n_lambda": L, "shared_jacobian_path": pf.shared_jacobian_path,
+                       "parallelism": f"replicas x{world} (one independent filter per GPU)"},
+            "rmse": rmse, "resample_rate": float(np.mean(res.flags)),
+            "host_tracker_ms_per_step": t_tr * 1e3 / K, "device_ms_per_step": dev_s * 1e3 / K,
+            "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "pf::ledh::k_flow_shared<40,10,L96> + weight/resample/moment pipeline",
+                         "flops_per_particle_step": ledh_flops_per_particle(nx, nz, L)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    pf.close()
+    if dist:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(wl, Z, mean0, cov0):
@@ -200,6 +317,9 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.workload == "ledh":
+        return main_ledh(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+                         int(os.environ.get("LOCAL_RANK", "0")))
     wl = WORKLOADS[args.workload]()
     K = args.steps if args.steps is not None else wl.defaults[0]
     W = args.warmup if args.warmup is not None else wl.defaults[1]

@@ -24,7 +24,8 @@ static pf_status lfail(pf_status code, const std::string& msg) {
 
 // size (doubles) of the shared-path flow table, TLay<nx, nz>::size(L)
 static size_t TLayHost(int nx, int nz, int L) {
-  return (size_t)(nx + nz) + (size_t)L * (size_t)(nx * nz + nz * nz + nx + nz + 1);
+  return (size_t)(nx + nz) + (size_t)L * (size_t)(nx * nz + nz * nz + nx + nz + 1) +
+         (size_t)(nx + nx * nz + nz + nz * nz + 1);
 }
 #define LCHK(expr)                                                                          \
   do {                                                                                      \
@@ -38,21 +39,25 @@ struct LOps {
   hipError_t (*flow_shared)(const FlowParams&, hipStream_t);
   hipError_t (*flow_wave)(const FlowParams&, int, hipStream_t);
   hipError_t (*normalise_chain)(const WParams&, hipStream_t);  // tile_max, exp_sum, normalise, decide
-  hipError_t (*resample)(const WParams&, bool commit, hipStream_t);
+  hipError_t (*resample)(const WParams&, hipStream_t);
   hipError_t (*stats)(const WParams&, bool cov, hipStream_t);
   hipError_t (*init)(double*, double*, const double*, const double*, const double*, int64_t, int64_t, uint64_t,
                      uint32_t, hipStream_t);
+  void (*prepare)();
 };
 
 template <int NX, int NZ, int TK, int OK>
 struct LL {
   static hipError_t setup(const FlowParams& p, double* table, int L, hipStream_t s) {
-    hipLaunchKernelGGL((k_setup<NX, NZ>), dim3(L), dim3(TB), 0, s, p, table);
+    hipLaunchKernelGGL((k_setup<NX, NZ>), dim3(L), dim3(SB), 0, s, p, table);
+    const size_t lds = (size_t)L * (TLay<NX, NZ>::PJ) * sizeof(double);
+    hipLaunchKernelGGL((k_compose<NX, NZ>), dim3(1), dim3(SB), lds, s, table, p.lams, L, p.dlam);
     return hipGetLastError();
   }
   static hipError_t flow_shared(const FlowParams& p, hipStream_t s) {
     if constexpr (OK == PF_OBS_LINEAR) {
-      hipLaunchKernelGGL((k_flow_shared<NX, NZ, TK>), dim3((unsigned)((p.N + TB - 1) / TB)), dim3(TB), 0, s, p);
+      const int64_t threads = p.N * Grp<NX>::GL;
+      hipLaunchKernelGGL((k_flow_affine<NX, NZ, TK>), dim3((unsigned)((threads + TB - 1) / TB)), dim3(TB), 0, s, p);
       return hipGetLastError();
     } else {
       return hipErrorInvalidValue;
@@ -63,27 +68,35 @@ struct LL {
     return hipGetLastError();
   }
   static hipError_t normalise_chain(const WParams& p, hipStream_t s) {
+    if (p.N <= SMALL_N) {
+      hipLaunchKernelGGL(k_weights_small, dim3(1), dim3(WB), 0, s, p);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_tile_max, dim3(p.G), dim3(TB), 0, s, p);
     hipLaunchKernelGGL(k_exp_sum, dim3(p.G), dim3(TB), 0, s, p);
     hipLaunchKernelGGL(k_normalise, dim3(p.G), dim3(TB), 0, s, p);
     hipLaunchKernelGGL(k_decide, dim3(1), dim3(TB), 0, s, p, 2);
-    return hipGetLastError();
-  }
-  static hipError_t resample(const WParams& p, bool commit, hipStream_t s) {
-    const unsigned gn = (unsigned)((p.N + TB - 1) / TB);
     hipLaunchKernelGGL(k_cdf, dim3(p.G), dim3(TB), 0, s, p, 2);
-    hipLaunchKernelGGL((k_gather<NX>), dim3(gn), dim3(TB), 0, s, p);
-    if (commit) hipLaunchKernelGGL((k_commit<NX>), dim3(gn), dim3(TB), 0, s, p);
     return hipGetLastError();
   }
-  static hipError_t stats(const WParams& p, bool cov, hipStream_t s) {
-    hipLaunchKernelGGL((k_mean_part<NX>), dim3(p.G), dim3(TB), 0, s, p);
-    hipLaunchKernelGGL((k_mean<NX>), dim3(1), dim3(TB), 0, s, p);
-    if (cov) {
-      hipLaunchKernelGGL((k_cov_part<NX>), dim3(p.Gc), dim3(TB), 0, s, p);
-      hipLaunchKernelGGL((k_cov<NX>), dim3(1), dim3(TB), 0, s, p);
-    }
+  // ancestors + gather into x_out / w_out, or copy-through when the decision was "no resample"
+  static hipError_t resample(const WParams& p, hipStream_t s) {
+    const size_t lds = p.N <= GCAP ? (size_t)p.N * sizeof(double) : 0;
+    hipLaunchKernelGGL((k_gather<NX>), dim3((unsigned)((p.N + TB - 1) / TB)), dim3(TB), lds, s, p);
     return hipGetLastError();
+  }
+  // posterior mean / cov (ledh.py:209, 217-224): one-pass shifted partials + final
+  static hipError_t stats(const WParams& p, bool cov, hipStream_t s) {
+    (void)cov;
+    hipLaunchKernelGGL((k_mom_part<NX>), dim3(p.Gc), dim3(TB), 0, s, p);
+    constexpr int NOUT = NX + NX * (NX + 1) / 2;
+    hipLaunchKernelGGL((k_mom_final<NX>), dim3((NOUT + TB - 1) / TB), dim3(TB), 0, s, p);
+    return hipGetLastError();
+  }
+  static void prepare() {
+    (void)hipFuncSetAttribute((const void*)k_gather<NX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(GCAP * sizeof(double)));
+    (void)hipFuncSetAttribute((const void*)k_compose<NX, NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
   }
   static hipError_t init(double* x, double* w, const double* mean0, const double* Lc, const double* eps, int64_t N,
                          int64_t Npad, uint64_t seed, uint32_t epoch, hipStream_t s) {
@@ -102,6 +115,7 @@ struct LL {
     o.resample = &resample;
     o.stats = &stats;
     o.init = &init;
+    o.prepare = &prepare;
     return o;
   }
 };
@@ -195,6 +209,7 @@ struct pf_ledh_handle {
   // device buffers
   double *x = nullptr, *x_alt = nullptr, *w = nullptr, *w_alt = nullptr, *lw = nullptr;
   double *tmax = nullptr, *tsum = nullptr, *trec = nullptr, *cdf = nullptr, *stat = nullptr, *mean = nullptr;
+  double* mean_prev = nullptr;  // shift of the one-pass moments (ping-pong with mean)
   double *cpart = nullptr, *Pm = nullptr, *Pk = nullptr, *z = nullptr, *u = nullptr, *vbuf = nullptr;
   double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
 };
@@ -241,6 +256,7 @@ WParams w_params(pf_ledh_handle* h) {
   p.cdf = h->cdf;
   p.stat = h->stat;
   p.mean = h->mean;
+  p.shift = h->mean_prev;
   p.cpart = h->cpart;
   p.o_mean = p.o_cov = p.o_ess = nullptr;
   p.o_flag = nullptr;
@@ -278,16 +294,19 @@ pf_status enqueue_flow(pf_ledh_handle* h, const double* Pk, const double* z, con
 }
 
 // resample (flag on the device) + posterior moments of the current state
-pf_status enqueue_finish(pf_ledh_handle* h, const double* U, bool commit, double* o_mean, double* o_cov) {
+pf_status enqueue_finish(pf_ledh_handle* h, const double* U, double* o_mean, double* o_cov) {
   const uint32_t ep_res = ++h->epoch;
   WParams wp = w_params(h);
   wp.unif = U;
   wp.epoch = ep_res;
-  LCHK(h->ops->resample(wp, commit, h->stream));
+  LCHK(h->ops->resample(wp, h->stream));
+  std::swap(h->x, h->x_alt);
+  std::swap(h->w, h->w_alt);
   WParams sp = w_params(h);
   sp.o_mean = o_mean;
   sp.o_cov = o_cov;
   LCHK(h->ops->stats(sp, true, h->stream));
+  std::swap(h->mean, h->mean_prev);  // the new mean is the next moments' shift
   return PF_OK;
 }
 
@@ -364,6 +383,10 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
   h->N = o->n_particles;
   h->Npad = (h->N + 3) / 4 * 4;
   h->L = std::max(1, (int)o->n_lambda);                   // ledh.py:132
+  if ((size_t)h->L * (size_t)(nx * nz + nz * nz + nx + nz + 1) * 8 > 120 * 1024) {
+    delete h;
+    return lfail(PF_E_ARG, "n_lambda_steps too large for the staged flow table of this model");
+  }
   h->dlam = 1.0 / (double)h->L;                           // ledh.py:133
   double lam = 0.0;
   for (int j = 0; j < h->L; ++j) {                        // ledh.py:134-137
@@ -377,7 +400,7 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
   h->q_diag = is_diag(Qi.data(), nx);
   h->r_diag = is_diag(Ri.data(), nz);
   h->G = (int)((h->N + LT - 1) / LT);
-  h->Gc = (int)((h->N + CT - 1) / CT);
+  h->Gc = (int)((h->N + CT * CTS - 1) / (CT * CTS));
   auto bail = [&](const char* what) {
     pf_ledh_destroy(h);
     return lfail(PF_E_HIP, std::string("hipMalloc failed: ") + what);
@@ -388,7 +411,8 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
   struct A { double** p; size_t b; };
   A allocs[] = {{&h->x, xb}, {&h->x_alt, xb}, {&h->w, nb}, {&h->w_alt, nb}, {&h->lw, nb}, {&h->cdf, nb},
                 {&h->tmax, (size_t)h->G * 8}, {&h->tsum, (size_t)h->G * 8}, {&h->trec, (size_t)h->G * (2 + nx) * 8},
-                {&h->stat, 8 * 8}, {&h->mean, (size_t)nx * 8}, {&h->cpart, (size_t)h->Gc * NP * 8},
+                {&h->stat, 8 * 8}, {&h->mean, (size_t)nx * 8}, {&h->mean_prev, (size_t)nx * 8},
+                {&h->cpart, (size_t)h->Gc * (1 + nx + NP) * 8},
                 {&h->Pm, P.size() * 8}, {&h->Pk, (size_t)nx * nx * 8}, {&h->z, (size_t)nz * 8},
                 {&h->u, (size_t)nx * 8}, {&h->table, (size_t)TLayHost(nx, nz, h->L) * 8}, {&h->d_lams, (size_t)h->L * 8},
                 {&h->diagS, (size_t)h->L * nz * nz * 8}, {&h->out, (size_t)(nx + nx * nx + 2) * 8},
@@ -397,6 +421,9 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
     if (hipMalloc((void**)a.p, a.b) != hipSuccess) return bail("state");
   (void)hipMemset(h->x, 0, xb);
   (void)hipMemset(h->x_alt, 0, xb);
+  (void)hipMemset(h->mean, 0, (size_t)nx * 8);
+  (void)hipMemset(h->mean_prev, 0, (size_t)nx * 8);
+  ops->prepare();
   if (hipMemcpy(h->Pm, P.data(), P.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->d_lams, h->lams.data(), h->lams.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
     return bail("upload");
@@ -408,7 +435,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean,
+  for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -440,8 +467,9 @@ pf_status pf_ledh_init(pf_ledh_handle* h, const double* mean0, const double* cov
   sp.uniform = 1;
   sp.o_cov = h->out + nx;
   LCHK(h->ops->stats(sp, true, h->stream));
+  std::swap(h->mean, h->mean_prev);  // the new mean is the next moments' shift
   LCHK(hipStreamSynchronize(h->stream));
-  if (mean_out) LCHK(hipMemcpy(mean_out, h->mean, nx * 8, hipMemcpyDeviceToHost));
+  if (mean_out) LCHK(hipMemcpy(mean_out, h->mean_prev, nx * 8, hipMemcpyDeviceToHost));
   if (cov_out) LCHK(hipMemcpy(cov_out, h->out + nx, (size_t)nx * nx * 8, hipMemcpyDeviceToHost));
   h->initialized = true;
   h->pending = false;
@@ -489,7 +517,7 @@ pf_status pf_ledh_finish(pf_ledh_handle* h, const double* U, double* mean, doubl
     WParams wp = w_params(h);
     wp.unif = U ? h->unif : nullptr;
     wp.epoch = ep_res;
-    LCHK(h->ops->resample(wp, false, h->stream));
+    LCHK(h->ops->resample(wp, h->stream));
     std::swap(h->x, h->x_alt);
     std::swap(h->w, h->w_alt);
     h->pending = false;
@@ -497,8 +525,9 @@ pf_status pf_ledh_finish(pf_ledh_handle* h, const double* U, double* mean, doubl
   WParams sp = w_params(h);
   sp.o_cov = h->out + nx;
   LCHK(h->ops->stats(sp, true, h->stream));
+  std::swap(h->mean, h->mean_prev);  // the new mean is the next moments' shift
   LCHK(hipStreamSynchronize(h->stream));
-  if (mean) LCHK(hipMemcpy(mean, h->mean, nx * 8, hipMemcpyDeviceToHost));
+  if (mean) LCHK(hipMemcpy(mean, h->mean_prev, nx * 8, hipMemcpyDeviceToHost));
   if (cov) LCHK(hipMemcpy(cov, h->out + nx, (size_t)nx * nx * 8, hipMemcpyDeviceToHost));
   return PF_OK;
 }
@@ -578,7 +607,7 @@ pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, cons
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
                         df + t);
-      if (st == PF_OK) st = enqueue_finish(h, nullptr, true, dm + t * nx, dc + t * nx * nx);
+      if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
     }
     if (st != PF_OK) break;
     if (hipStreamSynchronize(h->stream) != hipSuccess) {

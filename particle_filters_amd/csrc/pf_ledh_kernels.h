@@ -12,12 +12,13 @@
 // That is O(nx nz^2 + nz^3) per particle and lambda instead of O(nx^3).
 //
 // Two flow kernels:
-//   k_flow_shared  h linear (L96 x[::k], linear test systems): H, e = c, and hence K, M, S, Gm,
-//                  the logdets and P H^T R^{-1}(z - e) are the SAME for every particle.
-//                  k_setup computes them once per lambda_j (one workgroup per j) into a
-//                  table; a particle then only carries observation-space vectors:
-//                  y = H eta, s_j = y + y0 + 2 lam_j H w_j, eta_L = eta0 + sum_j dlam (c + lam_j ac_j + Gm_j s_j).
-//                  One thread per particle, SoA loads/stores.
+//   k_flow_affine  h linear (L96 x[::k], linear test systems): H, e = c, and hence K, M, S, Gm,
+//                  the logdets and P H^T R^{-1}(z - e) are the SAME for every particle, so
+//                  the whole lambda integration is an affine map of eta0.  k_setup builds the
+//                  per-lambda_j matrices (one workgroup per j), k_compose folds the L steps
+//                  into eta_L = eta0 + d0 + D (H eta0); a particle then costs g, its noise,
+//                  two small mat-vecs and the weight.  4 lanes per particle (L96: 10
+//                  contiguous components per lane, RK4 neighbours by lane shuffles).
 //   k_flow_wave    any h with an analytic Jacobian (EXP_HALF, ACOUSTIC): one 64-lane
 //                  workgroup per particle (persistent over particles), the small dense
 //                  algebra in LDS with lanes over matrix entries.
@@ -46,7 +47,8 @@ namespace ledh {
 constexpr int TB = 256;    // block of the per-particle-thread and reduction kernels
 constexpr int LT = 1024;   // particles per reduction tile
 constexpr int MAXT = 1024; // tiles (N <= LT * MAXT)
-constexpr int CT = 128;    // particles per covariance tile
+constexpr int CT = 128;    // particles per covariance sub-tile (staged in LDS)
+constexpr int CTS = 1;     // sub-tiles per moments workgroup
 
 // ---------------------------------------------------------------------------
 // parameter layout (doubles)
@@ -77,7 +79,15 @@ struct TLay {
   static constexpr int HAC = AC + NX;        // NZ     H A_j c
   static constexpr int LD = HAC + NZ;        // 1      log|det(I + dlam A_j)|
   static constexpr int PJ = LD + 1;
-  static constexpr int size(int L) { return HEAD + L * PJ; }
+  // the composed flow (k_compose): eta_L = eta0 + d0 + D (H eta0), H eta_L = pL + QL (H eta0)
+  static constexpr int aff(int L) { return HEAD + L * PJ; }
+  static constexpr int D0 = 0;               // NX
+  static constexpr int DM = D0 + NX;         // NX*NZ
+  static constexpr int PL = DM + NX * NZ;    // NZ
+  static constexpr int QL = PL + NZ;         // NZ*NZ
+  static constexpr int TH = QL + NZ * NZ;    // 1  theta = sum_j log|det(I + dlam A_j)|
+  static constexpr int AFF_SIZE = TH + 1;
+  static constexpr int size(int L) { return aff(L) + AFF_SIZE; }
 };
 
 struct FlowParams {
@@ -150,6 +160,29 @@ __device__ __forceinline__ void g_thread(double* x, const double* __restrict__ P
     if (u) {
 #pragma unroll
       for (int a = 0; a < NX; ++a) x[a] += u[a];
+    }
+  }
+}
+
+// normals of the flat indices f0 .. f0+PER-1 (NumPy row-major order of an (N, nx) draw):
+// one Philox call per group of 4 consecutive flat indices
+template <int PER>
+__device__ __forceinline__ void normals_range(uint64_t seed, int64_t f0, uint32_t epoch, uint32_t stream, double* n) {
+  constexpr int GMAX = PER / 4 + 2;
+  const int64_t g0 = f0 >> 2, g1 = (f0 + PER - 1) >> 2;
+#pragma unroll
+  for (int gg = 0; gg < GMAX; ++gg) {
+    const int64_t g = g0 + gg;
+    if (g <= g1) {
+      const Normal4<double> q4 = normal4<double>(seed, (uint32_t)g, 0u, epoch, stream);
+      // flat index 4g + e lands in slot 4g + e - f0 = 4 gg + e - (f0 & 3)
+      const int sh = (int)(f0 & 3);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+          if (4 * gg + e - sh == j) n[j] = q4.v[e];
+      }
     }
   }
 }
@@ -294,66 +327,67 @@ struct SetupSmem {
   static constexpr int SIZE = FAC + NZ;
 };
 
+constexpr int SB = 256;  // setup / compose workgroup
 template <int NX, int NZ>
-__global__ void __launch_bounds__(TB) k_setup(FlowParams p, double* table) {
+__global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   using SM = SetupSmem<NX, NZ>;
   __shared__ double sm[SM::SIZE];
   const int t = threadIdx.x, j = blockIdx.x;
   const double* __restrict__ Pm = p.Pm;
-  for (int q = t; q < NX * NX; q += TB) sm[SM::P + q] = p.Pk[q];
-  for (int q = t; q < NZ * NX; q += TB) sm[SM::H + q] = Pm[L::H + q];
-  for (int q = t; q < NZ * NZ; q += TB) sm[SM::R + q] = Pm[L::R + q];
+  for (int q = t; q < NX * NX; q += SB) sm[SM::P + q] = p.Pk[q];
+  for (int q = t; q < NZ * NX; q += SB) sm[SM::H + q] = Pm[L::H + q];
+  for (int q = t; q < NZ * NZ; q += SB) sm[SM::R + q] = Pm[L::R + q];
   __syncthreads();
   // K = P H^T
-  for (int q = t; q < NX * NZ; q += TB) {
+  for (int q = t; q < NX * NZ; q += SB) {
     const int d = q / NZ, k = q - d * NZ;
     double acc = 0.0;
     for (int e = 0; e < NX; ++e) acc += sm[SM::P + d * NX + e] * sm[SM::H + k * NX + e];
     sm[SM::K + q] = acc;
   }
   // r = R^{-1} (z - e), e = h(eta) - H eta = c for a linear h
-  for (int k = t; k < NZ; k += TB) {
+  for (int k = t; k < NZ; k += SB) {
     double acc = 0.0;
     for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - Pm[L::C + l]);
     sm[SM::RV + k] = acc;
   }
   __syncthreads();
   // M = H K ; c = K r
-  for (int q = t; q < NZ * NZ; q += TB) {
+  for (int q = t; q < NZ * NZ; q += SB) {
     const int k = q / NZ, l = q - k * NZ;
     double acc = 0.0;
     for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::K + d * NZ + l];
     sm[SM::M + q] = acc;
   }
-  for (int d = t; d < NX; d += TB) {
+  for (int d = t; d < NX; d += SB) {
     double acc = 0.0;
     for (int k = 0; k < NZ; ++k) acc += sm[SM::K + d * NZ + k] * sm[SM::RV + k];
     sm[SM::CV + d] = acc;
   }
   __syncthreads();
-  for (int k = t; k < NZ; k += TB) {
+  for (int k = t; k < NZ; k += SB) {
     double acc = 0.0;
     for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::CV + d];
     sm[SM::HC + k] = acc;
   }
   const double lam = p.lams[j];
   // S = lam M + R -> [S | I]
-  for (int q = t; q < NZ * 2 * NZ; q += TB) {
+  for (int q = t; q < NZ * 2 * NZ; q += SB) {
     const int r = q / (2 * NZ), c = q - r * 2 * NZ;
     sm[SM::AUG + q] = c < NZ ? lam * sm[SM::M + r * NZ + c] + sm[SM::R + r * NZ + c] : (c - NZ == r ? 1.0 : 0.0);
   }
   __syncthreads();
   if (p.diagS)
-    for (int q = t; q < NZ * NZ; q += TB) p.diagS[(int64_t)j * NZ * NZ + q] = sm[SM::AUG + (q / NZ) * 2 * NZ + q % NZ];
+    for (int q = t; q < NZ * NZ; q += SB) p.diagS[(int64_t)j * NZ * NZ + q] = sm[SM::AUG + (q / NZ) * 2 * NZ + q % NZ];
   __syncthreads();
   double S_ld;
   int S_sg;
   block_gauss_jordan(sm + SM::AUG, NZ, sm + SM::FAC, &S_ld, &S_sg);
   const double ld = flow_logdet<NX, NZ>(sm + SM::M, sm + SM::R, lam, p.dlam, S_ld, S_sg, sm + SM::T, sm + SM::FAC);
   // Gm = -1/2 K S^{-1}
-  for (int q = t; q < NX * NZ; q += TB) {
+  for (int q = t; q < NX * NZ; q += SB) {
     const int d = q / NZ, l = q - d * NZ;
     double acc = 0.0;
     for (int k = 0; k < NZ; ++k) acc += sm[SM::K + d * NZ + k] * sm[SM::AUG + k * 2 * NZ + NZ + l];
@@ -361,109 +395,289 @@ __global__ void __launch_bounds__(TB) k_setup(FlowParams p, double* table) {
   }
   __syncthreads();
   double* tj = table + T::HEAD + (int64_t)j * T::PJ;
-  for (int d = t; d < NX; d += TB) {
+  for (int d = t; d < NX; d += SB) {
     double acc = 0.0;
     for (int l = 0; l < NZ; ++l) acc += sm[SM::GM + d * NZ + l] * sm[SM::HC + l];
     sm[SM::AC + d] = acc;
     tj[T::AC + d] = acc;
   }
-  for (int q = t; q < NX * NZ; q += TB) tj[T::GM + q] = sm[SM::GM + q];
+  for (int q = t; q < NX * NZ; q += SB) tj[T::GM + q] = sm[SM::GM + q];
   __syncthreads();
-  for (int q = t; q < NZ * NZ; q += TB) {
+  for (int q = t; q < NZ * NZ; q += SB) {
     const int k = q / NZ, l = q - k * NZ;
     double acc = 0.0;
     for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::GM + d * NZ + l];
     tj[T::HGM + q] = acc;
   }
-  for (int k = t; k < NZ; k += TB) {
+  for (int k = t; k < NZ; k += SB) {
     double acc = 0.0;
     for (int d = 0; d < NX; ++d) acc += sm[SM::H + k * NX + d] * sm[SM::AC + d];
     tj[T::HAC + k] = acc;
   }
   if (t == 0) tj[T::LD] = ld;
   if (j == 0) {
-    for (int d = t; d < NX; d += TB) table[T::Cv + d] = sm[SM::CV + d];
-    for (int k = t; k < NZ; k += TB) table[T::HC + k] = sm[SM::HC + k];
+    for (int d = t; d < NX; d += SB) table[T::Cv + d] = sm[SM::CV + d];
+    for (int k = t; k < NZ; k += SB) table[T::HC + k] = sm[SM::HC + k];
   }
 }
 
 // ---------------------------------------------------------------------------
-// k_flow_shared: one thread per particle (linear h)
+// k_compose: with a linear h the flow ODE d eta / d lambda = A(lambda) eta + b(lambda; eta0)
+// has particle-independent coefficients, so lambda-stepping it (ledh.py:136-171) is an
+// affine map of eta0.  In observation space (y = H eta, y0 = H eta0), with per-step
+//   Hw_j = Hc + lam_j HAc_j + HGm_j y0,   s_j = y_j + y0 + 2 lam_j Hw_j,
+//   y_{j+1} = y_j + dlam (Hc + lam_j HAc_j + HGm_j s_j),
+//   eta_{j+1} = eta_j + dlam (c + lam_j Ac_j + Gm_j s_j),
+// every s_j = a_j + B_j y0 and y_j = p_j + Q_j y0 with shared a_j, B_j, p_j, Q_j, hence
+//   eta_L = eta0 + d0 + D y0,   y_L = pL + QL y0.
+// One workgroup composes the L steps (NZ^3 + NX NZ^2 per step).
 // ---------------------------------------------------------------------------
+template <int NX, int NZ>
+__global__ void __launch_bounds__(SB) k_compose(double* table, const double* lams, int L, double dlam) {
+  using T = TLay<NX, NZ>;
+  __shared__ double Qm[NZ * NZ], B[NZ * NZ], D[NX * NZ], pv[NZ], a[NZ], d0[NX], hd[T::HEAD];
+  extern __shared__ double tall[];  // [L][PJ]: the whole per-lambda table, staged once
+  const int t = threadIdx.x;
+  double* af = table + T::aff(L);
+  for (int q = t; q < NZ * NZ; q += SB) Qm[q] = (q / NZ == q % NZ) ? 1.0 : 0.0;
+  for (int q = t; q < NX * NZ; q += SB) D[q] = 0.0;
+  for (int k = t; k < NZ; k += SB) pv[k] = 0.0;
+  for (int d = t; d < NX; d += SB) d0[d] = 0.0;
+  for (int q = t; q < T::HEAD; q += SB) hd[q] = table[q];
+  for (int q = t; q < L * T::PJ; q += SB) tall[q] = table[T::HEAD + q];
+  double theta = 0.0;
+  __syncthreads();
+  for (int j = 0; j < L; ++j) {
+    const double lam = lams[j];
+    const double* tjs = tall + (int64_t)j * T::PJ;
+    // a = p + 2 lam hw_a ; B = Q + I + 2 lam HGm
+    for (int k = t; k < NZ; k += SB) a[k] = pv[k] + 2.0 * lam * (hd[T::HC + k] + lam * tjs[T::HAC + k]);
+    for (int q = t; q < NZ * NZ; q += SB)
+      B[q] = (Qm[q] + ((q / NZ == q % NZ) ? 1.0 : 0.0)) + 2.0 * lam * tjs[T::HGM + q];
+    __syncthreads();
+    // p += dlam (hw_a + HGm a) ; Q += dlam HGm B ; d0 += dlam (c + lam Ac + Gm a) ; D += dlam Gm B
+    for (int k = t; k < NZ; k += SB) {
+      double acc = hd[T::HC + k] + lam * tjs[T::HAC + k];
+      for (int l = 0; l < NZ; ++l) acc += tjs[T::HGM + k * NZ + l] * a[l];
+      pv[k] += dlam * acc;
+    }
+    for (int q = t; q < NZ * NZ; q += SB) {
+      const int k = q / NZ, m = q - k * NZ;
+      double acc = 0.0;
+      for (int l = 0; l < NZ; ++l) acc += tjs[T::HGM + k * NZ + l] * B[l * NZ + m];
+      Qm[q] += dlam * acc;
+    }
+    for (int d = t; d < NX; d += SB) {
+      double acc = hd[T::Cv + d] + lam * tjs[T::AC + d];
+      for (int l = 0; l < NZ; ++l) acc += tjs[T::GM + d * NZ + l] * a[l];
+      d0[d] += dlam * acc;
+    }
+    for (int q = t; q < NX * NZ; q += SB) {
+      const int d = q / NZ, m = q - d * NZ;
+      double acc = 0.0;
+      for (int l = 0; l < NZ; ++l) acc += tjs[T::GM + d * NZ + l] * B[l * NZ + m];
+      D[q] += dlam * acc;
+    }
+    theta += tjs[T::LD];
+    __syncthreads();
+  }
+  for (int d = t; d < NX; d += SB) af[T::D0 + d] = d0[d];
+  for (int q = t; q < NX * NZ; q += SB) af[T::DM + q] = D[q];
+  for (int k = t; k < NZ; k += SB) af[T::PL + k] = pv[k];
+  for (int q = t; q < NZ * NZ; q += SB) af[T::QL + q] = Qm[q];
+  if (t == 0) af[T::TH] = theta;
+}
+
+// ---------------------------------------------------------------------------
+// k_flow_affine: GL lanes per particle (PER = NX / GL components each), linear h
+// ---------------------------------------------------------------------------
+template <int NX>
+struct Grp {
+  static constexpr int GL = NX >= 16 ? 4 : 1;  // lanes per particle
+  static constexpr int PER = (NX + GL - 1) / GL;
+};
+
+// acc[j] += sum_e C[a_j][e] vec_e over the group-distributed vector (e <= a_j if lower),
+// streaming the components through lane shuffles instead of materialising the vector
+template <int NX>
+__device__ __forceinline__ void group_rows(const double* loc, const double* __restrict__ C, int q, int base,
+                                           double* acc, bool lower) {
+  constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+#pragma unroll
+  for (int r = 0; r < GL; ++r) {
+#pragma unroll
+    for (int jj = 0; jj < PER; ++jj) {
+      const double val = (GL == 1) ? loc[jj] : __shfl(loc[jj], base + r);
+      const int e = r * PER + jj;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int a = q * PER + j;
+        if (a < NX && e < NX && (!lower || e <= a)) acc[j] += C[a * NX + e] * val;
+      }
+    }
+  }
+}
+
+template <int GL>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 template <int NX, int NZ, int TK>
-__global__ void __launch_bounds__(TB) k_flow_shared(FlowParams p) {
+__global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
-  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (i >= p.N) return;
+  constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  const int64_t tid = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const int64_t i = tid / GL;
+  if (i >= p.N) return;  // whole groups leave together
+  const int q = (int)(tid % GL);
+  const int lane = threadIdx.x & 63;
+  const int base = lane - q;
   const double* __restrict__ Pm = p.Pm;
-  const double* __restrict__ tb = p.table;
-  double x[NX];
+  const double* __restrict__ af = p.table + T::aff(p.L);
+  double x[PER];
 #pragma unroll
-  for (int d = 0; d < NX; ++d) x[d] = p.x_in[(int64_t)d * p.Npad + i];
-  g_thread<NX, NZ, TK>(x, Pm, p.u);  // x <- g(x_{k-1}, u)
-  double v[NX];
-  noise_thread<NX, NZ>(p, i, v);
-  // eta0 = g(x) + v, parked in x_out (re-read at the end)
+  for (int j = 0; j < PER; ++j) {
+    const int a = q * PER + j;
+    x[j] = a < NX ? p.x_in[(int64_t)a * p.Npad + i] : 0.0;
+  }
+  // ---- g(x_{k-1}, u) ------------------------------------------------------------
+  double gx[PER];
+  if constexpr (TK == PF_TRANS_L96) {
+    static_assert(NX % GL == 0 && PER >= 2, "L96 lane groups hold >= 2 contiguous components each");
+    const double F = Pm[L::EX], dt = Pm[L::EX + 1];
+    const int nxt = base + (q + 1) % GL, prv = base + (q + GL - 1) % GL;
+    auto rhs = [&](const double* y, double* k) {
+      // neighbours across the lane boundary: y[a+1] from the next lane, y[a-1], y[a-2] from the previous
+      const double nx0 = GL == 1 ? y[0] : __shfl(y[0], nxt);
+      const double pv1 = GL == 1 ? y[PER - 1] : __shfl(y[PER - 1], prv);
+      const double pv2 = GL == 1 ? y[PER - 2] : __shfl(y[PER - 2], prv);
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const double yp1 = j + 1 < PER ? y[j + 1] : nx0;
+        const double ym1 = j >= 1 ? y[j - 1] : pv1;
+        const double ym2 = j >= 2 ? y[j - 2] : (j == 1 ? pv1 : pv2);
+        k[j] = (yp1 - ym2) * ym1 - y[j] + F;
+      }
+    };
+    double k[PER], acc[PER], tmp[PER];
+    rhs(x, k);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { acc[j] = k[j]; tmp[j] = x[j] + 0.5 * dt * k[j]; }
+    rhs(tmp, k);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { acc[j] += 2.0 * k[j]; tmp[j] = x[j] + 0.5 * dt * k[j]; }
+    rhs(tmp, k);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { acc[j] += 2.0 * k[j]; tmp[j] = x[j] + dt * k[j]; }
+    rhs(tmp, k);
+    const double h6 = dt / 6.0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) gx[j] = x[j] + h6 * (acc[j] + k[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) gx[j] = 0.0;
+    group_rows<NX>(x, Pm + L::A, q, base, gx, false);
+  }
+  if (p.u) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int a = q * PER + j;
+      if (a < NX) gx[j] += p.u[a];
+    }
+  }
+  // ---- process noise v ------------------------------------------------------------
+  double v[PER];
+  if (p.noise == PF_NOISE_HOST) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int a = q * PER + j;
+      v[j] = a < NX ? p.v_host[i * NX + a] : 0.0;
+    }
+  } else if (p.noise == PF_NOISE_DEVICE) {
+    double n[PER];
+    normals_range<PER>(p.seed, i * NX + q * PER, p.epoch, STREAM_PROCESS, n);
+    if (p.q_diag) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int a = q * PER + j;
+        v[j] = a < NX ? Pm[L::LQ + a * NX + a] * n[j] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) v[j] = 0.0;
+      group_rows<NX>(n, Pm + L::LQ, q, base, v, true);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[j] = 0.0;
+  }
+  // ---- eta0, y0 = H eta0 (group all-reduce), the composed flow ----------------------
+  double e0[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) e0[j] = gx[j] + v[j];
   double y0[NZ];
 #pragma unroll
-  for (int k = 0; k < NZ; ++k) y0[k] = 0.0;
+  for (int k = 0; k < NZ; ++k) {
+    double acc = 0.0;
 #pragma unroll
-  for (int d = 0; d < NX; ++d) {
-    const double e0 = x[d] + v[d];
-    p.x_out[(int64_t)d * p.Npad + i] = e0;
-#pragma unroll
-    for (int k = 0; k < NZ; ++k) y0[k] += Pm[L::H + k * NX + d] * e0;
+    for (int j = 0; j < PER; ++j) {
+      const int a = q * PER + j;
+      if (a < NX) acc += Pm[L::H + k * NX + a] * e0[j];
+    }
+    y0[k] = group_sum<GL>(acc);
   }
-  const double den = quad_form<NX>(v, Pm + L::QI, p.q_diag != 0);
-  double y[NZ], delta[NX];
+  double dd[PER];  // eta - g(x) = v + delta
 #pragma unroll
-  for (int k = 0; k < NZ; ++k) y[k] = y0[k];
+  for (int j = 0; j < PER; ++j) {
+    const int a = q * PER + j;
+    if (a < NX) {
+      double acc = af[T::D0 + a];
 #pragma unroll
-  for (int d = 0; d < NX; ++d) delta[d] = 0.0;
-  double theta = 0.0;
-  const double dlam = p.dlam;
-  for (int j = 0; j < p.L; ++j) {
-    const double lam = p.lams[j];
-    const double* tj = tb + T::HEAD + (int64_t)j * T::PJ;
-    double s[NZ];
+      for (int k = 0; k < NZ; ++k) acc += af[T::DM + a * NZ + k] * y0[k];
+      p.x_out[(int64_t)a * p.Npad + i] = e0[j] + acc;
+      dd[j] = v[j] + acc;
+    } else {
+      dd[j] = 0.0;
+    }
+  }
+  // ---- log weight (ledh.py:186-190) -----------------------------------------------
+  double part = 0.0;
+  if (p.q_diag) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int a = q * PER + j;
+      if (a < NX) {
+        const double qi = Pm[L::QI + a * NX + a];
+        part += (-0.5 * (dd[j] * (qi * dd[j]))) - (-0.5 * (v[j] * (qi * v[j])));
+      }
+    }
+  } else {
+    double ta[PER], tb[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) ta[j] = tb[j] = 0.0;
+    group_rows<NX>(dd, Pm + L::QI, q, base, ta, false);
+    group_rows<NX>(v, Pm + L::QI, q, base, tb, false);
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (q * PER + j < NX) part += (-0.5 * (dd[j] * ta[j])) - (-0.5 * (v[j] * tb[j]));
+  }
+  part = group_sum<GL>(part);
+  if (q == 0) {
+    double ez[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-      double hw = tb[T::HC + k] + lam * tj[T::HAC + k];
+      double yl = af[T::PL + k];
 #pragma unroll
-      for (int l = 0; l < NZ; ++l) hw += tj[T::HGM + k * NZ + l] * y0[l];
-      s[k] = y[k] + y0[k] + 2.0 * lam * hw;
+      for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
+      ez[k] = p.z[k] - (yl + Pm[L::C + k]);
     }
-#pragma unroll
-    for (int k = 0; k < NZ; ++k) {
-      double q = tb[T::HC + k] + lam * tj[T::HAC + k];
-#pragma unroll
-      for (int l = 0; l < NZ; ++l) q += tj[T::HGM + k * NZ + l] * s[l];
-      y[k] += dlam * q;
-    }
-#pragma unroll
-    for (int d = 0; d < NX; ++d) {
-      double q = tb[T::Cv + d] + lam * tj[T::AC + d];
-#pragma unroll
-      for (int l = 0; l < NZ; ++l) q += tj[T::GM + d * NZ + l] * s[l];
-      delta[d] += dlam * q;
-    }
-    theta += tj[T::LD];
+    const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
+    p.lw[i] = (log(p.w_in[i] + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
   }
-  // eta = eta0 + delta; eta - g(x) = v + delta
-#pragma unroll
-  for (int d = 0; d < NX; ++d) {
-    const int64_t o = (int64_t)d * p.Npad + i;
-    p.x_out[o] = p.x_out[o] + delta[d];
-    v[d] += delta[d];
-  }
-  const double num_t = quad_form<NX>(v, Pm + L::QI, p.q_diag != 0);
-  double ez[NZ];
-#pragma unroll
-  for (int k = 0; k < NZ; ++k) ez[k] = p.z[k] - (y[k] + Pm[L::C + k]);
-  const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
-  const double lw0 = log(p.w_in[i] + 1e-300) + theta;
-  p.lw[i] = lw0 + ((-0.5 * num_t) + (-0.5 * like) - (-0.5 * den));
 }
 
 // ---------------------------------------------------------------------------
@@ -778,8 +992,9 @@ struct WParams {
   double* trec;        // [G][2 + NX]  sum w, sum w^2, sum w x (per tile)
   double* cdf;         // [N]
   double* stat;        // [8]: ess, flag, sw, ...
-  double* mean;        // [NX]
-  double* cpart;       // [Gc][NX(NX+1)/2]
+  double* mean;        // [NX] the new posterior mean
+  const double* shift; // [NX] the previous mean (shift of the one-pass moments)
+  double* cpart;       // [Gc][1 + NX + NX(NX+1)/2]
   double* o_mean;      // output mean [NX] (nullable)
   double* o_cov;       // output cov [NX][NX] (nullable)
   double* o_ess;       // output ess (nullable)
@@ -899,119 +1114,227 @@ __global__ void __launch_bounds__(TB) k_cdf(WParams p, int rec_w) {
   }
 }
 
-// ancestors: idx_i = first j with (U + i)/N < cdf_j (ledh.py:28-37), clamped; gather x, w = 1/N
+// ancestors: idx_i = first j with (U + i)/N < cdf_j (ledh.py:28-37), clamped; gather x, w = 1/N.
+// Without a resample decision the kernel copies x, w through, so the caller can swap
+// the ping-pong buffers unconditionally (device-decided resampling in pf_ledh_run).
+constexpr int64_t GCAP = 16384;  // CDF entries staged in LDS by k_gather (128 KiB)
 template <int NX>
 __global__ void __launch_bounds__(TB) k_gather(WParams p) {
-  if (p.stat[1] == 0.0) return;
+  extern __shared__ double cs[];
   const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (i >= p.N) return;
-  const double U = p.unif ? p.unif[0] : uniform53(p.seed, 0u, 0u, p.epoch);
-  const double pos = (U + (double)i) / (double)p.N;
-  int64_t lo = 0, hi = p.N;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (pos < p.cdf[mid]) hi = mid; else lo = mid + 1;
+  const bool res = p.stat[1] != 0.0;
+  const bool staged = res && p.N <= GCAP;
+  if (staged) {
+    for (int64_t k = threadIdx.x; k < p.N; k += TB) cs[k] = p.cdf[k];
+    __syncthreads();
   }
-  const int64_t a = lo < p.N ? lo : p.N - 1;
+  if (i >= p.N) return;
+  int64_t a = i;
+  double wi;
+  if (res) {
+    const double U = p.unif ? p.unif[0] : uniform53(p.seed, 0u, 0u, p.epoch);
+    const double pos = (U + (double)i) / (double)p.N;
+    const double* C = staged ? cs : p.cdf;
+    int64_t lo = 0, hi = p.N;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (pos < C[mid]) hi = mid; else lo = mid + 1;
+    }
+    a = lo < p.N ? lo : p.N - 1;
+    wi = 1.0 / (double)p.N;
+  } else {
+    wi = p.w[i];
+  }
 #pragma unroll
   for (int d = 0; d < NX; ++d) p.x_out[(int64_t)d * p.Npad + i] = p.x_in[(int64_t)d * p.Npad + a];
-  p.w_out[i] = 1.0 / (double)p.N;
+  p.w_out[i] = wi;
 }
 
-// after a device-decided resample: copy the gathered set back (x_out -> x_in, w_out -> w)
-template <int NX>
-__global__ void __launch_bounds__(TB) k_commit(WParams p) {
-  if (p.stat[1] == 0.0) return;
-  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (i >= p.N) return;
+// the whole weight step in one workgroup for N <= SMALL_N: max, exp, normalise (ledh.py:191-195),
+// ESS and decision (ledh.py:39-41, 201-203), and the systematic-resampling CDF.
+constexpr int WB = 1024;
+constexpr int64_t SMALL_N = 65536;
+__device__ __forceinline__ double wave_incl_scan64(double v, int lane) {
 #pragma unroll
-  for (int d = 0; d < NX; ++d) p.x_in[(int64_t)d * p.Npad + i] = p.x_out[(int64_t)d * p.Npad + i];
-  p.w[i] = p.w_out[i];
-}
-
-// weighted mean, part 1: per tile sum w, sum w x  (ledh.py:217-220)
-template <int NX>
-__global__ void __launch_bounds__(TB) k_mean_part(WParams p) {
-  __shared__ double red[TB / 64];
-  const int b = blockIdx.x, t = threadIdx.x;
-  const int64_t o0 = (int64_t)b * LT, o1 = min(o0 + LT, p.N);
-  double a[1 + NX];
-#pragma unroll
-  for (int q = 0; q < 1 + NX; ++q) a[q] = 0.0;
-  for (int64_t i = o0 + t; i < o1; i += TB) {
-    const double wi = p.uniform ? 1.0 / (double)p.N : p.w[i];
-    a[0] += wi;
-#pragma unroll
-    for (int d = 0; d < NX; ++d) a[1 + d] += p.x_in[(int64_t)d * p.Npad + i] * wi;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(v, o);
+    if (lane >= o) v += t;
   }
-#pragma unroll
-  for (int q = 0; q < 1 + NX; ++q) {
-    const double s = block_reduce_sum(a[q], red);
-    if (t == 0) p.trec[(int64_t)b * (1 + NX) + q] = s;
-  }
+  return v;
 }
-
-template <int NX>
-__global__ void __launch_bounds__(TB) k_mean(WParams p) {
-  __shared__ double red[TB / 64];
-  const int t = threadIdx.x;
-  double sw = 0.0;
-  for (int k = t; k < p.G; k += TB) sw += p.trec[(int64_t)k * (1 + NX)];
-  sw = block_reduce_sum(sw, red);
-  for (int d = 0; d < NX; ++d) {
-    double s = 0.0;
-    for (int k = t; k < p.G; k += TB) s += p.trec[(int64_t)k * (1 + NX) + 1 + d];
-    s = block_reduce_sum(s, red);
-    if (t == 0) {
-      p.mean[d] = s / sw;
-      if (p.o_mean) p.o_mean[d] = s / sw;
+__global__ void __launch_bounds__(WB) k_weights_small(WParams p) {
+  __shared__ double red[WB / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double m = -INFINITY;
+  for (int64_t i = t; i < p.N; i += WB) m = fmax(m, p.lw[i]);
+  const double M = block_reduce_max(m, red);
+  double s = 0.0;
+  for (int64_t i = t; i < p.N; i += WB) {
+    const double e = exp(p.lw[i] - M);
+    p.w[i] = e;
+    s += e;
+  }
+  const double S = block_reduce_sum(s, red);
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t i = t; i < p.N; i += WB) {
+    const double wi = p.w[i] / S;
+    p.w[i] = wi;
+    a0 += wi;
+    a1 += wi * wi;
+  }
+  const double sw = block_reduce_sum(a0, red);
+  const double sw2 = block_reduce_sum(a1, red);
+  const double ess = 1.0 / (sw2 / (sw * sw));
+  const int flag = (p.ratio > 0.0) && (ess < p.ratio * (double)p.N);
+  if (flag) {  // cdf = cumsum(w / sum w), one block scan per round of WB consecutive weights
+    double run = 0.0;
+    for (int64_t r0 = 0; r0 < p.N; r0 += WB) {
+      const int64_t i = r0 + t;
+      const double wi = i < p.N ? p.w[i] : 0.0;
+      const double inc = wave_incl_scan64(wi, lane);
+      if (lane == 63) red[wv] = inc;
+      __syncthreads();
+      double off = 0.0, tot = 0.0;
+      for (int k = 0; k < WB / 64; ++k) {
+        if (k < wv) off += red[k];
+        tot += red[k];
+      }
+      if (i < p.N) p.cdf[i] = (run + (off + inc)) / sw;
+      run += tot;
+      __syncthreads();
     }
   }
-  if (t == 0) p.stat[3] = sw;
+  if (t == 0) {
+    p.stat[0] = ess;
+    p.stat[1] = flag;
+    p.stat[2] = sw;
+    if (p.o_ess) *p.o_ess = ess;
+    if (p.o_flag) *p.o_flag = flag;
+  }
 }
 
-// weighted covariance, part 1: per tile of CT particles, sum w (x-m)(x-m)^T (upper triangle)
+// K simultaneous block sums (one pass): result valid in every thread
+template <int K>
+__device__ __forceinline__ void block_sum_multi(double (&v)[K], double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = (int)(blockDim.x >> 6);
+#pragma unroll
+  for (int f = 0; f < K; ++f) v[f] = wave_sum64(v[f]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int f = 0; f < K; ++f) red[w * K + f] = v[f];
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < K; ++f) {
+    double s = 0.0;
+    for (int k = 0; k < nw; ++k) s += red[k * K + f];
+    v[f] = s;
+  }
+  __syncthreads();
+}
+
+// Posterior moments (ledh.py:217-224) in one pass over the particles, shifted by the
+// previous mean c (so sum w (x-c)(x-c)^T / sw - (m-c)(m-c)^T loses nothing to cancellation):
+// per tile of CT particles the partial sums  sum w | sum w (x-c) | sum w (x-c)(x-c)^T (upper).
 template <int NX>
-__global__ void __launch_bounds__(TB) k_cov_part(WParams p) {
-  constexpr int NP = NX * (NX + 1) / 2;
+struct Mom {
+  static constexpr int NP = NX * (NX + 1) / 2;
+  static constexpr int E = 1 + NX + NP;
+};
+__device__ __forceinline__ void pair_of(int q, int NX, int* d, int* e) {
+  int dd = 0, rem = q;
+  while (rem >= NX - dd) { rem -= NX - dd; ++dd; }
+  *d = dd;
+  *e = dd + rem;
+}
+template <int NX>
+__global__ void __launch_bounds__(TB) k_mom_part(WParams p) {
+  using MM = Mom<NX>;
+  constexpr int EPT = (MM::E + TB - 1) / TB;  // entries per thread
   __shared__ double xs[CT * NX];
   __shared__ double ws[CT];
   const int b = blockIdx.x, t = threadIdx.x;
-  const int64_t o0 = (int64_t)b * CT;
-  const int n = (int)min((int64_t)CT, p.N - o0);
-  for (int q = t; q < CT * NX; q += TB) {
-    const int j = q / NX, d = q - j * NX;
-    xs[q] = j < n ? p.x_in[(int64_t)d * p.Npad + o0 + j] - p.mean[d] : 0.0;
+  double acc[EPT];
+  int dq[EPT], eq[EPT];
+#pragma unroll
+  for (int r = 0; r < EPT; ++r) {
+    acc[r] = 0.0;
+    const int q = t + r * TB;
+    if (q > NX && q < MM::E) pair_of(q - 1 - NX, NX, &dq[r], &eq[r]);
+    else dq[r] = eq[r] = 0;
   }
-  for (int j = t; j < CT; j += TB) ws[j] = j < n ? (p.uniform ? 1.0 / (double)p.N : p.w[o0 + j]) : 0.0;
-  __syncthreads();
-  for (int q = t; q < NP; q += TB) {
-    // q -> (d, e) with d <= e, row-major upper triangle
-    int d = 0, rem = q;
-    while (rem >= NX - d) { rem -= NX - d; ++d; }
-    const int e = d + rem;
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc += (xs[j * NX + d] * ws[j]) * xs[j * NX + e];
-    p.cpart[(int64_t)b * NP + q] = acc;
+  for (int sub = 0; sub < CTS; ++sub) {
+    const int64_t o0 = ((int64_t)b * CTS + sub) * CT;
+    const int n = (int)max((int64_t)0, min((int64_t)CT, p.N - o0));
+    __syncthreads();
+    for (int q = t; q < CT * NX; q += TB) {
+      const int j = q / NX, d = q - j * NX;
+      xs[q] = j < n ? p.x_in[(int64_t)d * p.Npad + o0 + j] - p.shift[d] : 0.0;
+    }
+    for (int j = t; j < CT; j += TB) ws[j] = j < n ? (p.uniform ? 1.0 / (double)p.N : p.w[o0 + j]) : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      const int q = t + r * TB;
+      if (q >= MM::E) continue;
+      double a = 0.0;
+      if (q == 0) {
+        for (int j = 0; j < n; ++j) a += ws[j];
+      } else if (q <= NX) {
+        for (int j = 0; j < n; ++j) a += ws[j] * xs[j * NX + q - 1];
+      } else {
+        for (int j = 0; j < n; ++j) a += (xs[j * NX + dq[r]] * ws[j]) * xs[j * NX + eq[r]];
+      }
+      acc[r] += a;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < EPT; ++r) {
+    const int q = t + r * TB;
+    if (q < MM::E) p.cpart[(int64_t)b * MM::E + q] = acc[r];
   }
 }
 
+// sum of entry q over the Gc tile partials, fixed order
+__device__ __forceinline__ double part_sum(const double* cpart, int Gc, int E, int q) {
+  double acc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc[r] = 0.0;
+  int k = 0;
+  for (; k + 8 <= Gc; k += 8) {
+    double v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = cpart[(int64_t)(k + r) * E + q];  // 8 loads in flight
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] += v[r];
+  }
+  for (; k < Gc; ++k) acc[0] += cpart[(int64_t)k * E + q];
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// mean = c + s1/sw, cov = s2/sw - (s1/sw)(s1/sw)^T; one thread per output entry
 template <int NX>
-__global__ void __launch_bounds__(TB) k_cov(WParams p) {
-  constexpr int NP = NX * (NX + 1) / 2;
-  const int t = threadIdx.x;
-  const double sw = p.stat[3];
-  for (int q = t; q < NP; q += TB) {
-    int d = 0, rem = q;
-    while (rem >= NX - d) { rem -= NX - d; ++d; }
-    const int e = d + rem;
-    double acc = 0.0;
-    for (int k = 0; k < p.Gc; ++k) acc += p.cpart[(int64_t)k * NP + q];
-    const double c = acc / sw;
-    if (p.o_cov) {
-      p.o_cov[d * NX + e] = c;
-      p.o_cov[e * NX + d] = c;
-    }
+__global__ void __launch_bounds__(TB) k_mom_final(WParams p) {
+  using MM = Mom<NX>;
+  const int q = blockIdx.x * TB + threadIdx.x;
+  if (q >= NX + MM::NP) return;
+  const double sw = part_sum(p.cpart, p.Gc, MM::E, 0);
+  if (q < NX) {
+    const double m = p.shift[q] + part_sum(p.cpart, p.Gc, MM::E, 1 + q) / sw;
+    p.mean[q] = m;
+    if (p.o_mean) p.o_mean[q] = m;
+    if (q == 0) p.stat[3] = sw;
+    return;
+  }
+  int d, e;
+  pair_of(q - NX, NX, &d, &e);
+  const double md = part_sum(p.cpart, p.Gc, MM::E, 1 + d) / sw;
+  const double me = part_sum(p.cpart, p.Gc, MM::E, 1 + e) / sw;
+  const double c = part_sum(p.cpart, p.Gc, MM::E, 1 + NX + (q - NX)) / sw - md * me;
+  if (p.o_cov) {
+    p.o_cov[d * NX + e] = c;
+    p.o_cov[e * NX + d] = c;
   }
 }
 
@@ -1023,13 +1346,7 @@ __global__ void __launch_bounds__(TB) k_init(double* x, double* w, const double*
   const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
   if (i >= N) return;
   double n[NX];
-  if (!eps) {
-#pragma unroll
-    for (int d = 0; d < NX; ++d) {
-      const int64_t f = i * NX + d;
-      n[d] = normal4<double>(seed, (uint32_t)(f >> 2), 0u, epoch, STREAM_INIT).v[f & 3];
-    }
-  }
+  if (!eps) normals_range<NX>(seed, i * NX, epoch, STREAM_INIT, n);
 #pragma unroll
   for (int d = 0; d < NX; ++d) {
     double e;
