@@ -111,6 +111,7 @@ struct pf_handle {
   uint32_t epoch = 1;         // Philox epoch counter (one per predict, one per update)
   uint32_t ep_res = 0;        // epoch reserved by the last update for its resample
   bool chol_q_ok = true;
+  int lq_local = 0, lj_local = 0;  // chol(Q) / 0.001 chol(Q) block-diagonal in nx/4 blocks (k_step_grp)
   std::vector<double> Pd;     // params (double)
   // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
   unsigned long long* rsync = nullptr;
@@ -134,6 +135,10 @@ bool choose_geometry(pf_handle* h) {
   if ((h->N + tile - 1) / tile > MAXG) tile = (h->N + MAXG - 1) / MAXG;
   tile = (tile + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
   if (tile > h->N) tile = (h->N + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
+  // many replicates: grow small tiles while the grid exceeds ~4096 workgroups (every workgroup
+  // reduces all G records of its replicate in the prologue: O(G^2 R) record reads)
+  while (!env && (int64_t)h->R * ((h->N + tile - 1) / tile) > 4096 && tile < 256 && tile * 2 <= h->ops->tile_max)
+    tile *= 2;
   if (tile > h->ops->tile_max) return false;
   h->tile = (int)tile;
   h->G = (int)((h->N + tile - 1) / tile);
@@ -172,6 +177,8 @@ StepParams base_params(pf_handle* h) {
   p.regularize = h->regularize;
   p.r_diag = h->r_diag;
   p.rep_base = h->rep_base;
+  p.lq_local = h->lq_local;
+  p.lj_local = h->lj_local;
   p.out_step = -1;
   p.out_post_step = -1;
   p.z_rs = h->nz;
@@ -471,6 +478,17 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   h->esz = o->precision == PF_PRECISION_FP64 ? 8 : 4;
   h->r_diag = r_diag;
   h->chol_q_ok = qok;
+  if (nx >= 16 && nx % 4 == 0) {  // block-diagonality in the lane blocks of k_step_grp (SGrp<NX>)
+    const int per = nx / ((nx >= 32 && nx % 8 == 0) ? 8 : 4);
+    auto local = [&](int off) {
+      for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j)
+          if (i / per != j / per && P[off + i * nx + j] != 0.0) return 0;
+      return 1;
+    };
+    h->lq_local = local(lay_LQ);
+    h->lj_local = local(lay_LJ);
+  }
   h->Pd = P;
   if (!choose_geometry(h)) {
     delete h;

@@ -218,6 +218,7 @@ struct StepParams {
   int do_predict, do_update, allow_gather, regularize, r_diag;
   int force_gather;       // resample regardless of Neff (ParticleFilter._resample after its own test)
   int rep_base;           // global id of replicate 0 of this launch (Philox counter word)
+  int lq_local, lj_local; // chol(Q) / jitter factor block-diagonal in the lane blocks of k_step_grp
 };
 
 struct Head {

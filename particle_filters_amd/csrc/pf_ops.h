@@ -11,6 +11,7 @@
 
 #include "pf_kernels.h"
 #include "pf_resident.h"
+#include "pf_step_grp.h"
 
 namespace pf {
 
@@ -40,7 +41,15 @@ template <typename Real, int NX, int NZ, int TK, int OK>
 struct Launch {
   static constexpr int BS = StepTraits<Real, NX, NZ, TK, OK>::BS;
   static hipError_t step(const StepParams& p, dim3 grid, size_t smem, hipStream_t s) {
-    hipLaunchKernelGGL((k_step<Real, NX, NZ, TK, OK>), grid, dim3(BS), smem, s, p);
+    if constexpr (SGrp<NX>::ON) {  // large state: 4 lanes per particle (pf_step_grp.h)
+      const bool rd = p.r_diag != 0, ql = p.lq_local != 0 && p.lj_local != 0;
+      if (rd && ql) hipLaunchKernelGGL((k_step_grp<Real, NX, NZ, TK, OK, true, true>), grid, dim3(256), smem, s, p);
+      else if (rd) hipLaunchKernelGGL((k_step_grp<Real, NX, NZ, TK, OK, true, false>), grid, dim3(256), smem, s, p);
+      else if (ql) hipLaunchKernelGGL((k_step_grp<Real, NX, NZ, TK, OK, false, true>), grid, dim3(256), smem, s, p);
+      else hipLaunchKernelGGL((k_step_grp<Real, NX, NZ, TK, OK, false, false>), grid, dim3(256), smem, s, p);
+    } else {
+      hipLaunchKernelGGL((k_step<Real, NX, NZ, TK, OK>), grid, dim3(BS), smem, s, p);
+    }
     return hipGetLastError();
   }
   static hipError_t finalize(const StepParams& p, int R, hipStream_t s) {
@@ -75,7 +84,8 @@ struct Launch {
     o.rec_size = Rec<NX>::SIZE;
     o.ch = StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.tile_max = StepTraits<Real, NX, NZ, TK, OK>::TILE_MAX;
-    o.tile_min = BS * StepTraits<Real, NX, NZ, TK, OK>::CH;
+    // large states (k_step_grp): one particle per lane group per round -> 256 / GL particles
+    o.tile_min = SGrp<NX>::ON ? 256 / SGrp<NX>::GL : BS * StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.psize = ParamLayout<NX, NZ>::SIZE;
     o.step = &step;
     o.finalize = &finalize;
@@ -88,8 +98,15 @@ struct Launch {
   }
   static void prepare() {
     // allow up to 160 KiB of dynamic LDS for the tile CDF
-    (void)hipFuncSetAttribute((const void*)k_step<Real, NX, NZ, TK, OK>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if constexpr (SGrp<NX>::ON) {
+      for (const void* fn : {(const void*)k_step_grp<Real, NX, NZ, TK, OK, true, true>,
+                             (const void*)k_step_grp<Real, NX, NZ, TK, OK, true, false>,
+                             (const void*)k_step_grp<Real, NX, NZ, TK, OK, false, true>,
+                             (const void*)k_step_grp<Real, NX, NZ, TK, OK, false, false>})
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);  // + static z[NZ]
+    } else
+      (void)hipFuncSetAttribute((const void*)k_step<Real, NX, NZ, TK, OK>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k_cdf<Real, NX, BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
   }
