@@ -222,18 +222,13 @@ def main_ledh(args, world, rank, local):
     Z = sim.observations[1:]
     pf, tracker = make()
     st = pf.init_from_gaussian(mean0, cov0)
-    pf.run(st, Z[:max(W, 1)])  # warm-up (same sequence as the timed run)
+    pf.run(st, Z[:max(W, 1)], tracker="device")  # warm-up (same sequence as the timed run)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    Ps = np.empty((K, nx, nx))
-    for t in range(K):  # the host tracker (never sees particles): run ahead over Z
-        _, P = tracker.predict()
-        Ps[t] = P
-        tracker.update(Z[W + t])
-    t_tr = time.perf_counter() - t0
-    res = pf.run(pf.state, Z[W:W + K], tracker_covs=Ps)
+    # the whole job on the device: EKF tracker (k_ekf_seq), all flow tables, then the T flow steps
+    res = pf.run(pf.state, Z[W:W + K], tracker="device")
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -242,7 +237,22 @@ def main_ledh(args, world, rank, local):
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    dev_s = elapsed - t_tr
+    # host-tracker variant (the reference's call pattern: tracker stepped in Python), for the record
+    pf2, tracker2 = make()
+    st2 = pf2.init_from_gaussian(mean0, cov0)
+    pf2.run(st2, Z[:max(W, 1)])
+    h0 = time.perf_counter()
+    Ps = np.empty((K, nx, nx))
+    for t in range(K):
+        _, P = tracker2.predict()
+        Ps[t] = P
+        tracker2.update(Z[W + t])
+    t_tr = time.perf_counter() - h0
+    pf2.run(pf2.state, Z[W:W + K], tracker_covs=Ps)
+    torch.cuda.synchronize()
+    t_host_total = time.perf_counter() - h0
+    pf2.close()
+    dev_s = elapsed
     rmse = res.rmse(sim.truth_traj[W + 1:W + K + 1])
     flops = ledh_flops_per_particle(nx, nz, L) * Np * K
     if rank == 0:
@@ -273,15 +283,17 @@ def main_ledh(args, world, rank, local):
             "dtype": "f64",
             "data": "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)",
             "config": {"workload": "LEDH particle-flow PF (BASELINE config 5): L96 d=40, N=1e4 particles, 8 lambda "
-                                   "steps, ESS-ratio 0.5 systematic resampling, EKF tracker (host, analytic RK4 "
-                                   "Jacobian), Philox process noise",
+                                   "steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
+                                   "(analytic RK4 Jacobian), Philox process noise",
                        "n_particles": Np, "n_lambda": L, "shared_jacobian_path": pf.shared_jacobian_path,
                        "parallelism": f"replicas x{world} (one independent filter per GPU)"},
             "rmse": rmse, "resample_rate": float(np.mean(res.flags)),
-            "host_tracker_ms_per_step": t_tr * 1e3 / K, "device_ms_per_step": dev_s * 1e3 / K,
+            "host_tracker_variant": {"ms_per_step": t_host_total * 1e3 / K, "tracker_ms_per_step": t_tr * 1e3 / K,
+                                     "note": "EKF stepped on the host in NumPy, covariances uploaded, same device loop"},
             "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "pf::ledh::k_flow_shared<40,10,L96> + weight/resample/moment pipeline",
+                         "kernel": "whole LEDH job: k_ekf_seq + k_setup/k_compose + per step k_flow_affine, "
+                                   "k_weights_small, k_gather, k_mom_part, k_mom_final",
                          "flops_per_particle_step": ledh_flops_per_particle(nx, nz, L)},
             "cpu_baseline": cpu,
         }

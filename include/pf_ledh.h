@@ -8,9 +8,10 @@
  * one handle = one device + one stream, not re-entrant) are those of pf_engine.h.
  *
  * Arithmetic is fp64 (the reference's).  The Gaussian tracker (EKF/UKF,
- * ledh.py:13-16) stays on the host: it never sees the particles, so the caller
- * hands the engine its predicted covariance P_k per step (pf_ledh_step) or the
- * whole sequence P_1..P_T up front (pf_ledh_run).
+ * ledh.py:13-16) never sees the particles, so the caller hands the engine its
+ * predicted covariance P_k per step (pf_ledh_step) or the whole sequence P_1..P_T
+ * up front (pf_ledh_run) — or lets the engine run the EKF itself on the device
+ * (pf_ledh_run_ekf, pf_ledh_ekf_sequence).
  */
 #ifndef PF_LEDH_H
 #define PF_LEDH_H
@@ -86,6 +87,20 @@ pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const do
  * covs [T][nx][nx], ess [T], flags [T]. */
 pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T,
                       int32_t noise, double* means, double* covs, double* ess, uint8_t* flags);
+
+/* The Gaussian tracker on the device: the additive-noise EKF of extended_kalman_filter.py:164-241
+ * (predict x = g(x), P = G P G^T + Qt; update with S = H P H^T + Rt, K = P H^T S^-1, P = (I - K H) P)
+ * with the compiled model's analytic Jacobians, run over Z [T][nz] from (x0 [nx], P0 [nx][nx]).
+ * Ps [T][nx][nx] (host, nullable) gets the symmetrised predicted covariances the flow uses
+ * (ledh.py:105-106); x_final / P_final (nullable) the tracker's last posterior. */
+pf_status pf_ledh_ekf_sequence(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt,
+                               const double* Rt, const double* Z, int64_t T, double* Ps, double* x_final,
+                               double* P_final);
+
+/* pf_ledh_run with the device EKF as the tracker (no host work inside the run). */
+pf_status pf_ledh_run_ekf(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt, const double* Rt,
+                          const double* Z, const double* U, int64_t T, int32_t noise, double* means, double* covs,
+                          double* ess, uint8_t* flags, double* x_final, double* P_final);
 
 /* Measurement hooks: the handle's stream, synchronisation, and whether the last step used the
  * shared-Jacobian path. */

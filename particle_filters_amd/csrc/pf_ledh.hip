@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/pf_ledh.h"
+#include "pf_ledh_ekf.h"
 #include "pf_ledh_kernels.h"
 
 namespace pf {
@@ -35,7 +36,7 @@ static size_t TLayHost(int nx, int nz, int L) {
 
 struct LOps {
   int nx, nz, tk, ok, psize;
-  hipError_t (*setup)(const FlowParams&, double*, int, hipStream_t);
+  hipError_t (*setup)(const FlowParams&, double*, int, int, hipStream_t);  // (.., L, n_steps, ..)
   hipError_t (*flow_shared)(const FlowParams&, hipStream_t);
   hipError_t (*flow_wave)(const FlowParams&, int, hipStream_t);
   hipError_t (*normalise_chain)(const WParams&, hipStream_t);  // tile_max, exp_sum, normalise, decide
@@ -44,14 +45,18 @@ struct LOps {
   hipError_t (*init)(double*, double*, const double*, const double*, const double*, int64_t, int64_t, uint64_t,
                      uint32_t, hipStream_t);
   void (*prepare)();
+  hipError_t (*ekf)(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
+                    const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, hipStream_t);
 };
 
 template <int NX, int NZ, int TK, int OK>
 struct LL {
-  static hipError_t setup(const FlowParams& p, double* table, int L, hipStream_t s) {
-    hipLaunchKernelGGL((k_setup<NX, NZ>), dim3(L), dim3(SB), 0, s, p, table);
+  // flow tables of n_steps time steps at once (P_k, z_k, table_k strided by the FlowParams strides)
+  static hipError_t setup(const FlowParams& p, double* table, int L, int n_steps, hipStream_t s) {
+    hipLaunchKernelGGL((k_setup<NX, NZ>), dim3(L, n_steps), dim3(SB), 0, s, p, table);
     const size_t lds = (size_t)L * (TLay<NX, NZ>::PJ) * sizeof(double);
-    hipLaunchKernelGGL((k_compose<NX, NZ>), dim3(1), dim3(SB), lds, s, table, p.lams, L, p.dlam);
+    hipLaunchKernelGGL((k_compose<NX, NZ>), dim3(n_steps), dim3(SB), lds, s, table, p.lams, L, p.dlam,
+                       p.table_stride);
     return hipGetLastError();
   }
   static hipError_t flow_shared(const FlowParams& p, hipStream_t s) {
@@ -104,8 +109,14 @@ struct LL {
                        Npad, seed, epoch);
     return hipGetLastError();
   }
+  static hipError_t ekf(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
+                        const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, hipStream_t s) {
+    hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(EB), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out);
+    return hipGetLastError();
+  }
   static LOps make() {
     LOps o;
+    o.ekf = &ekf;
     o.nx = NX; o.nz = NZ; o.tk = TK; o.ok = OK;
     o.psize = Lay<NX, NZ>::SIZE;
     o.setup = &setup;
@@ -229,6 +240,7 @@ FlowParams flow_params(pf_ledh_handle* h, const double* Pk, const double* z, con
   p.u = u;
   p.v_host = v;
   p.table = h->table;
+  p.pk_stride = p.z_stride = p.table_stride = 0;
   p.lams = h->d_lams;
   p.diagS = diagS;
   p.N = h->N;
@@ -274,12 +286,14 @@ WParams w_params(pf_ledh_handle* h) {
 
 // flow + weights + decision of one step (ledh.py:104-203), all enqueued on h->stream
 pf_status enqueue_flow(pf_ledh_handle* h, const double* Pk, const double* z, const double* u, int noise,
-                       const double* v, double* diagS, double* o_ess, int32_t* o_flag) {
+                       const double* v, double* diagS, double* o_ess, int32_t* o_flag,
+                       const double* pre_table = nullptr) {
   const uint32_t ep_noise = ++h->epoch;
   FlowParams fp = flow_params(h, Pk, z, u, noise, v, diagS);
   fp.epoch = ep_noise;
   if (h->shared) {
-    LCHK(h->ops->setup(fp, h->table, h->L, h->stream));
+    if (pre_table) fp.table = pre_table;  // built for the whole run up front (pf_ledh_run)
+    else LCHK(h->ops->setup(fp, h->table, h->L, 1, h->stream));
     LCHK(h->ops->flow_shared(fp, h->stream));
   } else {
     int grid = (int)std::min<int64_t>(h->N, 256 * 16);
@@ -567,46 +581,93 @@ pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const do
   return PF_OK;
 }
 
-pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T, int32_t noise,
-                      double* means, double* covs, double* ess, uint8_t* flags) {
-  if (!h || !Ps || !Z) return lfail(PF_E_ARG, "null argument");
+}  // extern "C"
+
+namespace {
+
+// Device EKF spec: host arrays (x0, P0, Qt, Rt) or all null.
+struct EkfSpec {
+  const double *x0, *P0, *Qt, *Rt;
+  double *x_final, *P_final;
+};
+
+// The T loop (pf_ledh_run / pf_ledh_run_ekf): tracker covariances from the host (Ps) or from the
+// device EKF, all flow tables built up front, then flow -> weights -> resample -> moments per step.
+pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, const double* Z, const double* U, int64_t T,
+                   int32_t noise, double* means, double* covs, double* ess, uint8_t* flags) {
+  if (!h || !Z || (!Ps && !ekf)) return lfail(PF_E_ARG, "null argument");
   if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (noise != PF_NOISE_NONE && noise != PF_NOISE_DEVICE) return lfail(PF_E_ARG, "run: noise must be NONE or DEVICE");
   if (T <= 0) return PF_OK;
   LCHK(hipSetDevice(h->device));
   const int nx = h->nx, nz = h->nz;
-  std::vector<double> S((size_t)T * nx * nx);
-  for (int64_t t = 0; t < T; ++t)
-    for (int i = 0; i < nx; ++i)
-      for (int j = 0; j < nx; ++j)
-        S[(t * nx + i) * nx + j] = 0.5 * (Ps[(t * nx + i) * nx + j] + Ps[(t * nx + j) * nx + i]);
-  double *dP = nullptr, *dZ = nullptr, *dU = nullptr, *dm = nullptr, *dc = nullptr, *de = nullptr;
+  std::vector<double> S;
+  if (Ps) {
+    S.resize((size_t)T * nx * nx);
+    for (int64_t t = 0; t < T; ++t)
+      for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j)
+          S[(t * nx + i) * nx + j] = 0.5 * (Ps[(t * nx + i) * nx + j] + Ps[(t * nx + j) * nx + i]);  // ledh.py:106
+  }
+  double *dP = nullptr, *dZ = nullptr, *dU = nullptr, *dm = nullptr, *dc = nullptr, *de = nullptr, *dTab = nullptr;
+  double* dE = nullptr;  // EKF inputs / outputs: x0 | P0 | Qt | Rt | x_final | P_final
   int32_t* df = nullptr;
   auto cleanup = [&]() {
-    for (double* p : {dP, dZ, dU, dm, dc, de})
+    for (double* p : {dP, dZ, dU, dm, dc, de, dTab, dE})
       if (p) (void)hipFree(p);
     if (df) (void)hipFree(df);
   };
-  bool ok = hipMalloc((void**)&dP, S.size() * 8) == hipSuccess && hipMalloc((void**)&dZ, (size_t)T * nz * 8) == hipSuccess &&
+  const size_t ne = 2 * (size_t)nx + 3 * (size_t)nx * nx + (size_t)nz * nz;
+  bool ok = hipMalloc((void**)&dP, (size_t)T * nx * nx * 8) == hipSuccess &&
+            hipMalloc((void**)&dZ, (size_t)T * nz * 8) == hipSuccess &&
             (!U || hipMalloc((void**)&dU, (size_t)T * nx * 8) == hipSuccess) &&
             hipMalloc((void**)&dm, (size_t)T * nx * 8) == hipSuccess &&
             hipMalloc((void**)&dc, (size_t)T * nx * nx * 8) == hipSuccess &&
-            hipMalloc((void**)&de, (size_t)T * 8) == hipSuccess && hipMalloc((void**)&df, (size_t)T * 4) == hipSuccess;
+            hipMalloc((void**)&de, (size_t)T * 8) == hipSuccess && hipMalloc((void**)&df, (size_t)T * 4) == hipSuccess &&
+            (!ekf || hipMalloc((void**)&dE, ne * 8) == hipSuccess);
   if (!ok) {
     cleanup();
     return lfail(PF_E_HIP, "hipMalloc of run buffers failed");
   }
   pf_status st = PF_OK;
   do {
-    if (hipMemcpyAsync(dP, S.data(), S.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+    if ((Ps && hipMemcpyAsync(dP, S.data(), S.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
         hipMemcpyAsync(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
         (U && hipMemcpyAsync(dU, U, (size_t)T * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)) {
       st = lfail(PF_E_HIP, "upload of run inputs failed");
       break;
     }
+    double *ex0 = dE, *eP0 = dE + nx, *eQ = eP0 + nx * nx, *eR = eQ + nx * nx, *exf = eR + nz * nz, *ePf = exf + nx;
+    if (ekf) {
+      if (hipMemcpyAsync(ex0, ekf->x0, nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+          hipMemcpyAsync(eP0, ekf->P0, (size_t)nx * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+          hipMemcpyAsync(eQ, ekf->Qt, (size_t)nx * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+          hipMemcpyAsync(eR, ekf->Rt, (size_t)nz * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+          h->ops->ekf(h->Pm, ex0, eP0, eQ, eR, dZ, T, dP, exf, ePf, h->stream) != hipSuccess) {
+        st = lfail(PF_E_HIP, "run: device EKF launch failed");
+        break;
+      }
+    }
+    // the flow tables depend on (P_k, z_k) only, not on the particles: build all T at once
+    const size_t tsz = TLayHost(nx, nz, h->L);
+    if (h->shared) {
+      if (hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
+        st = lfail(PF_E_HIP, "hipMalloc of the run's flow tables failed");
+        break;
+      }
+      for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += 65535) {  // grid.y <= 65535 steps per launch
+        FlowParams fp = flow_params(h, dP + c0 * nx * nx, dZ + c0 * nz, nullptr, noise, nullptr, nullptr);
+        fp.pk_stride = (int64_t)nx * nx;
+        fp.z_stride = nz;
+        fp.table_stride = (int64_t)tsz;
+        if (h->ops->setup(fp, dTab + c0 * tsz, h->L, (int)std::min<int64_t>(65535, T - c0), h->stream) != hipSuccess)
+          st = lfail(PF_E_HIP, "run: batched flow-table launch failed");
+      }
+      if (st != PF_OK) break;
+    }
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
-                        df + t);
+                        df + t, dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
     }
     if (st != PF_OK) break;
@@ -618,7 +679,9 @@ pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, cons
     if ((means && hipMemcpy(means, dm, (size_t)T * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
         (covs && hipMemcpy(covs, dc, (size_t)T * nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
         (ess && hipMemcpy(ess, de, (size_t)T * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
-        hipMemcpy(fl.data(), df, (size_t)T * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        hipMemcpy(fl.data(), df, (size_t)T * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (ekf && ekf->x_final && hipMemcpy(ekf->x_final, exf, nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (ekf && ekf->P_final && hipMemcpy(ekf->P_final, ePf, (size_t)nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess)) {
       st = lfail(PF_E_HIP, "download of run outputs failed");
       break;
     }
@@ -627,6 +690,56 @@ pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, cons
   } while (false);
   cleanup();
   h->pending = false;
+  return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T, int32_t noise,
+                      double* means, double* covs, double* ess, uint8_t* flags) {
+  if (!Ps) return lfail(PF_E_ARG, "null argument");
+  return run_impl(h, Ps, nullptr, Z, U, T, noise, means, covs, ess, flags);
+}
+
+pf_status pf_ledh_run_ekf(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt, const double* Rt,
+                          const double* Z, const double* U, int64_t T, int32_t noise, double* means, double* covs,
+                          double* ess, uint8_t* flags, double* x_final, double* P_final) {
+  if (!x0 || !P0 || !Qt || !Rt) return lfail(PF_E_ARG, "null argument");
+  EkfSpec e{x0, P0, Qt, Rt, x_final, P_final};
+  return run_impl(h, nullptr, &e, Z, U, T, noise, means, covs, ess, flags);
+}
+
+pf_status pf_ledh_ekf_sequence(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt,
+                               const double* Rt, const double* Z, int64_t T, double* Ps, double* x_final,
+                               double* P_final) {
+  if (!h || !x0 || !P0 || !Qt || !Rt || !Z) return lfail(PF_E_ARG, "null argument");
+  if (T <= 0) return PF_OK;
+  LCHK(hipSetDevice(h->device));
+  const int nx = h->nx, nz = h->nz;
+  const size_t ne = 2 * (size_t)nx + 3 * (size_t)nx * nx + (size_t)nz * nz;
+  double *dE = nullptr, *dZ = nullptr, *dP = nullptr;
+  pf_status st = PF_OK;
+  if (hipMalloc((void**)&dE, ne * 8) != hipSuccess || hipMalloc((void**)&dZ, (size_t)T * nz * 8) != hipSuccess ||
+      hipMalloc((void**)&dP, (size_t)T * nx * nx * 8) != hipSuccess) {
+    st = lfail(PF_E_HIP, "hipMalloc of EKF buffers failed");
+  } else {
+    double *ex0 = dE, *eP0 = dE + nx, *eQ = eP0 + nx * nx, *eR = eQ + nx * nx, *exf = eR + nz * nz, *ePf = exf + nx;
+    if (hipMemcpy(ex0, x0, nx * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(eP0, P0, (size_t)nx * nx * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(eQ, Qt, (size_t)nx * nx * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(eR, Rt, (size_t)nz * nz * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        h->ops->ekf(h->Pm, ex0, eP0, eQ, eR, dZ, T, dP, exf, ePf, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess ||
+        (Ps && hipMemcpy(Ps, dP, (size_t)T * nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (x_final && hipMemcpy(x_final, exf, nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (P_final && hipMemcpy(P_final, ePf, (size_t)nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess))
+      st = lfail(PF_E_HIP, "device EKF failed");
+  }
+  for (double* p : {dE, dZ, dP})
+    if (p) (void)hipFree(p);
   return st;
 }
 

@@ -101,6 +101,7 @@ struct FlowParams {
   const double* u;      // [NX] or null
   const double* v_host; // [N][NX] or null
   const double* table;  // TLay (shared path)
+  int64_t pk_stride, z_stride, table_stride;  // batched k_setup / k_compose over steps (blockIdx.y / .x)
   const double* lams;   // [L]
   double* diagS;        // [L][NZ][NZ] or null (S of particle 0)
   int64_t N, Npad;
@@ -335,8 +336,13 @@ __global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
   using SM = SetupSmem<NX, NZ>;
   __shared__ double sm[SM::SIZE];
   const int t = threadIdx.x, j = blockIdx.x;
+  const int64_t step = blockIdx.y;  // batched over time steps (pf_ledh_run): P_k, z_k, table_k
+  const double* Pk = p.Pk + step * p.pk_stride;
+  const double* zk = p.z + step * p.z_stride;
+  table += step * p.table_stride;
+  double* diagS = gridDim.y == 1 ? p.diagS : nullptr;
   const double* __restrict__ Pm = p.Pm;
-  for (int q = t; q < NX * NX; q += SB) sm[SM::P + q] = p.Pk[q];
+  for (int q = t; q < NX * NX; q += SB) sm[SM::P + q] = Pk[q];
   for (int q = t; q < NZ * NX; q += SB) sm[SM::H + q] = Pm[L::H + q];
   for (int q = t; q < NZ * NZ; q += SB) sm[SM::R + q] = Pm[L::R + q];
   __syncthreads();
@@ -350,7 +356,7 @@ __global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
   // r = R^{-1} (z - e), e = h(eta) - H eta = c for a linear h
   for (int k = t; k < NZ; k += SB) {
     double acc = 0.0;
-    for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - Pm[L::C + l]);
+    for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (zk[l] - Pm[L::C + l]);
     sm[SM::RV + k] = acc;
   }
   __syncthreads();
@@ -379,8 +385,8 @@ __global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
     sm[SM::AUG + q] = c < NZ ? lam * sm[SM::M + r * NZ + c] + sm[SM::R + r * NZ + c] : (c - NZ == r ? 1.0 : 0.0);
   }
   __syncthreads();
-  if (p.diagS)
-    for (int q = t; q < NZ * NZ; q += SB) p.diagS[(int64_t)j * NZ * NZ + q] = sm[SM::AUG + (q / NZ) * 2 * NZ + q % NZ];
+  if (diagS)
+    for (int q = t; q < NZ * NZ; q += SB) diagS[(int64_t)j * NZ * NZ + q] = sm[SM::AUG + (q / NZ) * 2 * NZ + q % NZ];
   __syncthreads();
   double S_ld;
   int S_sg;
@@ -433,8 +439,10 @@ __global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
 // One workgroup composes the L steps (NZ^3 + NX NZ^2 per step).
 // ---------------------------------------------------------------------------
 template <int NX, int NZ>
-__global__ void __launch_bounds__(SB) k_compose(double* table, const double* lams, int L, double dlam) {
+__global__ void __launch_bounds__(SB) k_compose(double* table, const double* lams, int L, double dlam,
+                                                int64_t table_stride) {
   using T = TLay<NX, NZ>;
+  table += (int64_t)blockIdx.x * table_stride;  // batched over time steps
   __shared__ double Qm[NZ * NZ], B[NZ * NZ], D[NX * NZ], pv[NZ], a[NZ], d0[NX], hd[T::HEAD];
   extern __shared__ double tall[];  // [L][PJ]: the whole per-lambda table, staged once
   const int t = threadIdx.x;

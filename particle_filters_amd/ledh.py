@@ -260,18 +260,62 @@ class LEDHFlowPF:
                 conds.append(np.nan)
         return self._new_state(mean, cov, {"condition_numbers": conds})
 
+    def _device_tracker(self):
+        """(x, P, Qt, Rt) of a trackers.EKFTracker whose EKF runs this filter's own models."""
+        from . import trackers as TR
+
+        tr = self.tracker
+        if not (isinstance(tr, TR.EKFTracker) and tr.ekf.g is self.g and tr.ekf.h is self.h):
+            raise NotImplementedError("tracker='device' needs a trackers.EKFTracker over this filter's g and h")
+        c = lambda a: np.ascontiguousarray(np.asarray(a, float))  # noqa: E731
+        return c(tr.state.mean).reshape(self.nx), c(tr.state.cov).reshape(self.nx, self.nx), c(tr.ekf.Q), c(tr.ekf.R)
+
+    def tracker_covariances(self, Z: Array) -> Array:
+        """The device EKF (analytic Jacobians of the compiled model) over Z from the tracker's
+        current state: the symmetrised predicted covariances [T][nx][nx] the flow would use.
+        The tracker object is not advanced."""
+        x0, P0, Qt, Rt = self._device_tracker()
+        Z = np.ascontiguousarray(np.asarray(Z, float).reshape(-1, self.nz))
+        Ps = np.empty((Z.shape[0], self.nx, self.nx))
+        N.check(N.load().pf_ledh_ekf_sequence(self._h, N.dptr(x0), N.dptr(P0), N.dptr(Qt), N.dptr(Rt), N.dptr(Z),
+                                              Z.shape[0], N.dptr(Ps), None, None), "pf_ledh_ekf_sequence")
+        return Ps
+
     def run(self, state: PFState, Z: Array, U: Optional[Array] = None, *, process_noise: str = "device",
-            tracker_covs: Optional[Array] = None) -> LEDHRunResult:
+            tracker_covs: Optional[Array] = None, tracker: str = "host") -> LEDHRunResult:
         """The driver loop ``for t: state = step(state, Z[t])`` on the device with no host
-        synchronisation inside T.  The tracker is run ahead over Z (predict/update, the same
-        call sequence as the loop — it never sees the particles) unless ``tracker_covs``
-        [T][nx][nx] is given; process noise is Philox times chol(Q) (``"device"``) or zero
-        (``"none"``, the reference default); resampling uniforms come from Philox."""
+        synchronisation inside T.  ``tracker="host"``: the tracker object is run ahead over Z
+        (predict/update, the same call sequence as the loop — it never sees the particles)
+        unless ``tracker_covs`` [T][nx][nx] is given.  ``tracker="device"``: an EKFTracker over
+        this filter's models runs on the GPU (analytic Jacobians), and its object is advanced
+        to the final posterior afterwards.  Process noise is Philox times chol(Q)
+        (``"device"``) or zero (``"none"``, the reference default); resampling uniforms come
+        from Philox."""
         if process_noise not in ("device", "none"):
             raise ValueError("process_noise must be 'device' or 'none'")
+        if tracker not in ("host", "device"):
+            raise ValueError("tracker must be 'host' or 'device'")
         self._adopt(state)
         Z = np.ascontiguousarray(np.asarray(Z, float).reshape(-1, self.nz))
         T = Z.shape[0]
+        noise = N.PF_NOISE_DEVICE if process_noise == "device" else N.PF_NOISE_NONE
+        if tracker == "device":
+            from . import trackers as TR
+
+            x0, P0, Qt, Rt = self._device_tracker()
+            Uc = None if U is None else np.ascontiguousarray(np.asarray(U, float).reshape(T, self.nx))
+            means, covs = np.empty((T, self.nx)), np.empty((T, self.nx, self.nx))
+            ess, flags = np.empty(T), np.zeros(T, dtype=np.uint8)
+            xf, Pf = np.empty(self.nx), np.empty((self.nx, self.nx))
+            N.check(N.load().pf_ledh_run_ekf(self._h, N.dptr(x0), N.dptr(P0), N.dptr(Qt), N.dptr(Rt), N.dptr(Z),
+                                             N.dptr(Uc), T, noise, N.dptr(means), N.dptr(covs), N.dptr(ess),
+                                             flags.ctypes.data_as(N.C.POINTER(N.C.c_uint8)), N.dptr(xf), N.dptr(Pf)),
+                    "pf_ledh_run_ekf")
+            tr = self.tracker
+            tr.past_mean = xf.copy()  # approximate: the mean before the last predict is not kept
+            tr.state = TR.EKFState(mean=xf, cov=Pf, t=tr.state.t + T)
+            self._new_state(means[-1], covs[-1], {})
+            return LEDHRunResult(means, covs, ess, flags.astype(bool))
         if tracker_covs is None:
             Ps = np.empty((T, self.nx, self.nx))
             for t in range(T):
@@ -285,7 +329,6 @@ class LEDHFlowPF:
         covs = np.empty((T, self.nx, self.nx))
         ess = np.empty(T)
         flags = np.zeros(T, dtype=np.uint8)
-        noise = N.PF_NOISE_DEVICE if process_noise == "device" else N.PF_NOISE_NONE
         N.check(N.load().pf_ledh_run(self._h, N.dptr(Ps), N.dptr(Z), N.dptr(Uc), T, noise, N.dptr(means),
                                      N.dptr(covs), N.dptr(ess), flags.ctypes.data_as(N.C.POINTER(N.C.c_uint8))),
                 "pf_ledh_run")

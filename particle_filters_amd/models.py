@@ -82,6 +82,10 @@ class LinearTransition(Transition):
         y = self.A @ x if u is None else self.A @ x + u
         return y if v is None else y + v
 
+    def jacobian(self, x, u=None):
+        """dg/dx = A (the EKF's analytic Jacobian of g)."""
+        return self.A.copy()
+
 
 class SVTransition(LinearTransition):
     """Stochastic-volatility AR(1): ``g(x) = alpha * x`` (elementwise for vector alpha)."""

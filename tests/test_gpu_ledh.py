@@ -159,3 +159,47 @@ def test_large_l96_shared_vs_per_particle():
             ms.append(st.mean)
         out[flow] = np.array(ms)
     np.testing.assert_allclose(out["auto"], out["per_particle"], rtol=0, atol=1e-8)
+
+
+def device_tracked_filter(name, n_particles=2000, seed=11, rng_mode="device"):
+    """A filter whose EKFTracker runs the engine's own device models (analytic Jacobians)."""
+    om, gm, hm, g = case(name)
+    ekf = TR.ExtendedKalmanFilter(gm, hm, om.Q, om.R, jac_g=gm.jacobian, jac_h=hm.jacobian)
+    tracker = TR.EKFTracker(ekf, TR.EKFState(np.asarray(g["mean0"], float).copy(),
+                                             np.asarray(g["cov0"], float).copy(), 0))
+    cfg = LD.LEDHConfig(n_particles=n_particles, n_lambda_steps=int(g["n_lambda"]),
+                        resample_ess_ratio=float(g["ratio"]), rng=np.random.default_rng(seed))
+    pf = LD.LEDHFlowPF(tracker, gm, hm, hm.jacobian, M.GaussianTransitionDensity(gm, om.Q),
+                       M.GaussianLikelihood(hm, om.R), om.R, cfg, rng_mode=rng_mode)
+    return pf, tracker, ekf, g
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_device_ekf_matches_host_ekf(name):
+    """k_ekf_seq (the EKF of extended_kalman_filter.py:164-241 on the device) reproduces the
+    host EKF with the same analytic Jacobians: every symmetrised predicted covariance."""
+    pf, tracker, ekf, g = device_tracked_filter(name, n_particles=64)
+    Ps = pf.tracker_covariances(g["Z"])
+    host = TR.EKFTracker(ekf, TR.EKFState(np.asarray(g["mean0"], float).copy(),
+                                          np.asarray(g["cov0"], float).copy(), 0))
+    for t in range(len(g["Z"])):
+        _, P = host.predict()
+        ref = 0.5 * (P + P.T)
+        np.testing.assert_allclose(Ps[t], ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max(), err_msg=f"t={t}")
+        host.update(np.atleast_1d(g["Z"][t]))
+
+
+@pytest.mark.parametrize("name", ["l96", "acoustic"])
+def test_run_with_device_tracker_equals_host_tracker(name):
+    """run(tracker='device') == run(tracker_covs=<host EKF covariances>) on identical Philox
+    draws, to the rounding of the two EKF evaluations."""
+    pf1, tr1, ekf, g = device_tracked_filter(name)
+    st1 = pf1.init_from_gaussian(g["mean0"], g["cov0"])
+    r1 = pf1.run(st1, g["Z"], tracker="device")
+    pf2, tr2, _, _ = device_tracked_filter(name)
+    st2 = pf2.init_from_gaussian(g["mean0"], g["cov0"])
+    r2 = pf2.run(st2, g["Z"], tracker="host")
+    scale = max(1.0, float(np.abs(r2.means).max()))
+    np.testing.assert_array_equal(r1.flags, r2.flags)
+    np.testing.assert_allclose(r1.means, r2.means, rtol=0, atol=1e-8 * scale)
+    np.testing.assert_allclose(tr1.state.cov, tr2.state.cov, rtol=1e-9, atol=1e-12)
