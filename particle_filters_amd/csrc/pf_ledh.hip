@@ -74,7 +74,7 @@ struct LL {
   }
   static hipError_t normalise_chain(const WParams& p, hipStream_t s) {
     if (p.N <= SMALL_N) {
-      hipLaunchKernelGGL(k_weights_small, dim3(1), dim3(WB), 0, s, p);
+      hipLaunchKernelGGL(k_weights_small, dim3(1), dim3(WB), (size_t)p.N * sizeof(double), s, p);
       return hipGetLastError();
     }
     hipLaunchKernelGGL(k_tile_max, dim3(p.G), dim3(TB), 0, s, p);
@@ -95,13 +95,15 @@ struct LL {
     (void)cov;
     hipLaunchKernelGGL((k_mom_part<NX>), dim3(p.Gc), dim3(TB), 0, s, p);
     constexpr int NOUT = NX + NX * (NX + 1) / 2;
-    hipLaunchKernelGGL((k_mom_final<NX>), dim3((NOUT + TB - 1) / TB), dim3(TB), 0, s, p);
+    hipLaunchKernelGGL((k_mom_final<NX>), dim3((NOUT + MF_E - 1) / MF_E), dim3(MF_E * MF_P), 0, s, p);
     return hipGetLastError();
   }
   static void prepare() {
     (void)hipFuncSetAttribute((const void*)k_gather<NX>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(GCAP * sizeof(double)));
     (void)hipFuncSetAttribute((const void*)k_compose<NX, NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_weights_small, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(SMALL_N * sizeof(double)));
   }
   static hipError_t init(double* x, double* w, const double* mean0, const double* Lc, const double* eps, int64_t N,
                          int64_t Npad, uint64_t seed, uint32_t epoch, hipStream_t s) {

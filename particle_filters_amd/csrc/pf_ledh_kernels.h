@@ -1133,7 +1133,15 @@ __global__ void __launch_bounds__(TB) k_gather(WParams p) {
   const bool res = p.stat[1] != 0.0;
   const bool staged = res && p.N <= GCAP;
   if (staged) {
-    for (int64_t k = threadIdx.x; k < p.N; k += TB) cs[k] = p.cdf[k];
+    // batches of 8 independent loads, then the LDS stores (one memory round trip per batch)
+    for (int64_t k0 = threadIdx.x; k0 < p.N; k0 += 8 * TB) {
+      double v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = k0 + r * TB < p.N ? p.cdf[k0 + r * TB] : 0.0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (k0 + r * TB < p.N) cs[k0 + r * TB] = v[r];
+    }
     __syncthreads();
   }
   if (i >= p.N) return;
@@ -1161,7 +1169,7 @@ __global__ void __launch_bounds__(TB) k_gather(WParams p) {
 // the whole weight step in one workgroup for N <= SMALL_N: max, exp, normalise (ledh.py:191-195),
 // ESS and decision (ledh.py:39-41, 201-203), and the systematic-resampling CDF.
 constexpr int WB = 1024;
-constexpr int64_t SMALL_N = 65536;
+constexpr int64_t SMALL_N = 16384;  // LDS-staged weights (128 KiB) and 16 weights per thread in registers
 __device__ __forceinline__ double wave_incl_scan64(double v, int lane) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1170,46 +1178,58 @@ __device__ __forceinline__ double wave_incl_scan64(double v, int lane) {
   }
   return v;
 }
+constexpr int WPT = (int)(SMALL_N / WB);  // weights per thread kept in registers (N <= SMALL_N)
 __global__ void __launch_bounds__(WB) k_weights_small(WParams p) {
   __shared__ double red[WB / 64];
+  extern __shared__ double wl[];  // [N] normalised weights staged for the CDF scan
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double v[WPT];  // this thread's log weights, then weights: loaded once (coalesced i = t + r WB)
+#pragma unroll
+  for (int r = 0; r < WPT; ++r) {
+    const int64_t i = t + (int64_t)r * WB;
+    v[r] = i < p.N ? p.lw[i] : -INFINITY;
+  }
   double m = -INFINITY;
-  for (int64_t i = t; i < p.N; i += WB) m = fmax(m, p.lw[i]);
+#pragma unroll
+  for (int r = 0; r < WPT; ++r) m = fmax(m, v[r]);
   const double M = block_reduce_max(m, red);
   double s = 0.0;
-  for (int64_t i = t; i < p.N; i += WB) {
-    const double e = exp(p.lw[i] - M);
-    p.w[i] = e;
-    s += e;
+#pragma unroll
+  for (int r = 0; r < WPT; ++r) {
+    v[r] = (t + (int64_t)r * WB < p.N) ? exp(v[r] - M) : 0.0;
+    s += v[r];
   }
   const double S = block_reduce_sum(s, red);
   double a0 = 0.0, a1 = 0.0;
-  for (int64_t i = t; i < p.N; i += WB) {
-    const double wi = p.w[i] / S;
-    p.w[i] = wi;
-    a0 += wi;
-    a1 += wi * wi;
+#pragma unroll
+  for (int r = 0; r < WPT; ++r) {
+    const int64_t i = t + (int64_t)r * WB;
+    v[r] = v[r] / S;  // w /= sum(w) (ledh.py:195)
+    if (i < p.N) {
+      p.w[i] = v[r];
+      wl[i] = v[r];
+    }
+    a0 += v[r];
+    a1 += v[r] * v[r];
   }
   const double sw = block_reduce_sum(a0, red);
   const double sw2 = block_reduce_sum(a1, red);
   const double ess = 1.0 / (sw2 / (sw * sw));
   const int flag = (p.ratio > 0.0) && (ess < p.ratio * (double)p.N);
-  if (flag) {  // cdf = cumsum(w / sum w), one block scan per round of WB consecutive weights
-    double run = 0.0;
-    for (int64_t r0 = 0; r0 < p.N; r0 += WB) {
-      const int64_t i = r0 + t;
-      const double wi = i < p.N ? p.w[i] : 0.0;
-      const double inc = wave_incl_scan64(wi, lane);
-      if (lane == 63) red[wv] = inc;
-      __syncthreads();
-      double off = 0.0, tot = 0.0;
-      for (int k = 0; k < WB / 64; ++k) {
-        if (k < wv) off += red[k];
-        tot += red[k];
-      }
-      if (i < p.N) p.cdf[i] = (run + (off + inc)) / sw;
-      run += tot;
-      __syncthreads();
+  if (flag) {  // cdf = cumsum(w / sum w): contiguous chunks per thread from LDS, one block scan
+    const int64_t per = (p.N + WB - 1) / WB;
+    const int64_t i0 = (int64_t)t * per, i1 = min(i0 + per, p.N);
+    double c = 0.0;
+    for (int64_t i = i0; i < i1; ++i) c += wl[i];
+    const double inc = wave_incl_scan64(c, lane);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    double off = 0.0;
+    for (int k = 0; k < wv; ++k) off += red[k];
+    double run = off + inc - c;
+    for (int64_t i = i0; i < i1; ++i) {
+      run += wl[i];
+      p.cdf[i] = run / sw;
     }
   }
   if (t == 0) {
@@ -1256,51 +1276,82 @@ __device__ __forceinline__ void pair_of(int q, int NX, int* d, int* e) {
   *d = dd;
   *e = dd + rem;
 }
+// Register-blocked: thread = (4x4 block of the upper triangle, particle slice); the slices are
+// combined in LDS.  s0 and s1 by the first 1 + NX threads.
+template <int NX>
+struct MomBlk {
+  static constexpr int NB = (NX + 3) / 4;            // 4-wide blocks per dimension
+  static constexpr int NPAIR = NB * (NB + 1) / 2;     // upper-triangular block pairs
+  static constexpr int SL = NPAIR * 4 <= TB ? 4 : (NPAIR * 2 <= TB ? 2 : 1);  // particle slices
+  static constexpr int XW = NB * 4;                   // padded row width of the staged tile
+};
 template <int NX>
 __global__ void __launch_bounds__(TB) k_mom_part(WParams p) {
   using MM = Mom<NX>;
-  constexpr int EPT = (MM::E + TB - 1) / TB;  // entries per thread
-  __shared__ double xs[CT * NX];
+  using MB = MomBlk<NX>;
+  static_assert(MB::NPAIR * MB::SL <= TB, "block pairs x slices fit the workgroup");
+  __shared__ double xs[CT * MB::XW];
   __shared__ double ws[CT];
+  __shared__ double red[MB::SL][MB::NPAIR][16];
   const int b = blockIdx.x, t = threadIdx.x;
-  double acc[EPT];
-  int dq[EPT], eq[EPT];
-#pragma unroll
-  for (int r = 0; r < EPT; ++r) {
-    acc[r] = 0.0;
-    const int q = t + r * TB;
-    if (q > NX && q < MM::E) pair_of(q - 1 - NX, NX, &dq[r], &eq[r]);
-    else dq[r] = eq[r] = 0;
+  const int64_t o0 = (int64_t)b * CT;
+  const int n = (int)max((int64_t)0, min((int64_t)CT, p.N - o0));
+#pragma unroll 8
+  for (int q = t; q < CT * MB::XW; q += TB) {
+    const int j = q / MB::XW, d = q - j * MB::XW;
+    xs[q] = (j < n && d < NX) ? p.x_in[(int64_t)d * p.Npad + o0 + j] - p.shift[d] : 0.0;
   }
-  for (int sub = 0; sub < CTS; ++sub) {
-    const int64_t o0 = ((int64_t)b * CTS + sub) * CT;
-    const int n = (int)max((int64_t)0, min((int64_t)CT, p.N - o0));
-    __syncthreads();
-    for (int q = t; q < CT * NX; q += TB) {
-      const int j = q / NX, d = q - j * NX;
-      xs[q] = j < n ? p.x_in[(int64_t)d * p.Npad + o0 + j] - p.shift[d] : 0.0;
-    }
-    for (int j = t; j < CT; j += TB) ws[j] = j < n ? (p.uniform ? 1.0 / (double)p.N : p.w[o0 + j]) : 0.0;
-    __syncthreads();
+  for (int j = t; j < CT; j += TB) ws[j] = j < n ? (p.uniform ? 1.0 / (double)p.N : p.w[o0 + j]) : 0.0;
+  __syncthreads();
+  double* out = p.cpart + (int64_t)b * MM::E;
+  if (t <= NX) {  // s0 = sum w, s1_d = sum w (x_d - c_d)
+    double a = 0.0;
+    if (t == 0)
+      for (int j = 0; j < n; ++j) a += ws[j];
+    else
+      for (int j = 0; j < n; ++j) a += ws[j] * xs[j * MB::XW + t - 1];
+    out[t] = a;
+  }
+  const int pair = t % MB::NPAIR, sl = t / MB::NPAIR;
+  if (sl < MB::SL) {
+    int bi = 0, rem = pair;
+    while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
+    const int bj = bi + rem;
+    double acc[16];
 #pragma unroll
-    for (int r = 0; r < EPT; ++r) {
-      const int q = t + r * TB;
-      if (q >= MM::E) continue;
-      double a = 0.0;
-      if (q == 0) {
-        for (int j = 0; j < n; ++j) a += ws[j];
-      } else if (q <= NX) {
-        for (int j = 0; j < n; ++j) a += ws[j] * xs[j * NX + q - 1];
-      } else {
-        for (int j = 0; j < n; ++j) a += (xs[j * NX + dq[r]] * ws[j]) * xs[j * NX + eq[r]];
+    for (int k = 0; k < 16; ++k) acc[k] = 0.0;
+    for (int j = sl; j < n; j += MB::SL) {
+      const double* r = xs + j * MB::XW;
+      const double wj = ws[j];
+      double u[4], v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u[k] = r[4 * bi + k] * wj;
+        v[k] = r[4 * bj + k];
       }
-      acc[r] += a;
-    }
-  }
 #pragma unroll
-  for (int r = 0; r < EPT; ++r) {
-    const int q = t + r * TB;
-    if (q < MM::E) p.cpart[(int64_t)b * MM::E + q] = acc[r];
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) acc[k * 4 + l] += u[k] * v[l];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[sl][pair][k] = acc[k];
+  }
+  __syncthreads();
+  if (t < MB::NPAIR) {  // combine slices, scatter the block's upper-triangle entries
+    int bi = 0, rem = t;
+    while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
+    const int bj = bi + rem;
+    for (int k = 0; k < 4; ++k)
+      for (int l = 0; l < 4; ++l) {
+        const int d = 4 * bi + k, e = 4 * bj + l;
+        if (d >= NX || e >= NX || e < d) continue;
+        double a = 0.0;
+        for (int s2 = 0; s2 < MB::SL; ++s2) a += red[s2][t][k * 4 + l];
+        // upper-triangle index of (d, e): rows 0..d-1 hold NX - r entries each
+        const int q = d * NX - d * (d - 1) / 2 + (e - d);
+        out[1 + NX + q] = a;
+      }
   }
 }
 
@@ -1321,25 +1372,48 @@ __device__ __forceinline__ double part_sum(const double* cpart, int Gc, int E, i
   return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
-// mean = c + s1/sw, cov = s2/sw - (s1/sw)(s1/sw)^T; one thread per output entry
+// mean = c + s1/sw, cov = s2/sw - (s1/sw)(s1/sw)^T.  Workgroup = 16 output entries x 16 partial
+// lanes: lane p sums partials p, p+16, ... (independent loads), then an LDS tree per entry.
+constexpr int MF_E = 16, MF_P = 16;
 template <int NX>
-__global__ void __launch_bounds__(TB) k_mom_final(WParams p) {
+__global__ void __launch_bounds__(MF_E * MF_P) k_mom_final(WParams p) {
   using MM = Mom<NX>;
-  const int q = blockIdx.x * TB + threadIdx.x;
-  if (q >= NX + MM::NP) return;
-  const double sw = part_sum(p.cpart, p.Gc, MM::E, 0);
+  __shared__ double part[4][MF_E][MF_P + 1];
+  const int t = threadIdx.x, el = t / MF_P, pl = t % MF_P;
+  const int q = blockIdx.x * MF_E + el;  // output entry: q < NX mean, else cov pair
+  const bool live = q < NX + MM::NP;
+  int d = 0, e = 0;
+  if (live && q >= NX) pair_of(q - NX, NX, &d, &e);
+  const int src[4] = {0, 1 + (q < NX ? q : d), 1 + e, q >= NX ? 1 + NX + (q - NX) : 0};
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (live)
+    for (int k = pl; k < p.Gc; k += MF_P) {
+      double v[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) v[f] = p.cpart[(int64_t)k * MM::E + src[f]];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] += v[f];
+    }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) part[f][el][pl] = acc[f];
+  __syncthreads();
+  if (pl != 0 || !live) return;
+  double tot[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    double sum = 0.0;
+    for (int k = 0; k < MF_P; ++k) sum += part[f][el][k];
+    tot[f] = sum;
+  }
+  const double sw = tot[0];
   if (q < NX) {
-    const double m = p.shift[q] + part_sum(p.cpart, p.Gc, MM::E, 1 + q) / sw;
+    const double m = p.shift[q] + tot[1] / sw;
     p.mean[q] = m;
     if (p.o_mean) p.o_mean[q] = m;
     if (q == 0) p.stat[3] = sw;
     return;
   }
-  int d, e;
-  pair_of(q - NX, NX, &d, &e);
-  const double md = part_sum(p.cpart, p.Gc, MM::E, 1 + d) / sw;
-  const double me = part_sum(p.cpart, p.Gc, MM::E, 1 + e) / sw;
-  const double c = part_sum(p.cpart, p.Gc, MM::E, 1 + NX + (q - NX)) / sw - md * me;
+  const double c = tot[3] / sw - (tot[1] / sw) * (tot[2] / sw);
   if (p.o_cov) {
     p.o_cov[d * NX + e] = c;
     p.o_cov[e * NX + d] = c;
