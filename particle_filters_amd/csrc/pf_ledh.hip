@@ -218,6 +218,7 @@ struct pf_ledh_handle {
   bool initialized = false;
   bool pending = false;  // the last step decided to resample
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;  // tracker + flow tables, run ahead of the particle loop (pf_ledh_run_ekf)
   std::vector<double> lams;
   // device buffers
   double *x = nullptr, *x_alt = nullptr, *w = nullptr, *w_alt = nullptr, *lw = nullptr;
@@ -422,6 +423,7 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
     return lfail(PF_E_HIP, std::string("hipMalloc failed: ") + what);
   };
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return bail("stream");
+  if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) return bail("stream");
   const size_t xb = (size_t)nx * h->Npad * sizeof(double), nb = (size_t)h->N * sizeof(double);
   const int NP = nx * (nx + 1) / 2;
   struct A { double** p; size_t b; };
@@ -454,6 +456,8 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
   for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc})
     if (p) (void)hipFree(p);
+  if (h->side) (void)hipStreamSynchronize(h->side);
+  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -640,38 +644,68 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, cons
       break;
     }
     double *ex0 = dE, *eP0 = dE + nx, *eQ = eP0 + nx * nx, *eR = eQ + nx * nx, *exf = eR + nz * nz, *ePf = exf + nx;
+    const size_t tsz = TLayHost(nx, nz, h->L);
+    if (h->shared && hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
+      st = lfail(PF_E_HIP, "hipMalloc of the run's flow tables failed");
+      break;
+    }
+    // flow tables of steps [c0, c0 + n) (they depend on (P_k, z_k) only, not on the particles)
+    auto tables = [&](int64_t c0, int64_t n, hipStream_t s) -> bool {
+      if (!h->shared) return true;
+      FlowParams fp = flow_params(h, dP + c0 * nx * nx, dZ + c0 * nz, nullptr, noise, nullptr, nullptr);
+      fp.pk_stride = (int64_t)nx * nx;
+      fp.z_stride = nz;
+      fp.table_stride = (int64_t)tsz;
+      return h->ops->setup(fp, dTab + c0 * tsz, h->L, (int)n, s) == hipSuccess;
+    };
+    // Device tracker: the EKF and the tables run on the side stream CH steps at a time, ahead of the
+    // particle loop, which waits for each chunk's event (the tracker never needs the particles).
+    const int64_t CH = 16;
+    std::vector<hipEvent_t> evs;
     if (ekf) {
       if (hipMemcpyAsync(ex0, ekf->x0, nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
           hipMemcpyAsync(eP0, ekf->P0, (size_t)nx * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
           hipMemcpyAsync(eQ, ekf->Qt, (size_t)nx * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
           hipMemcpyAsync(eR, ekf->Rt, (size_t)nz * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-          h->ops->ekf(h->Pm, ex0, eP0, eQ, eR, dZ, T, dP, exf, ePf, h->stream) != hipSuccess) {
-        st = lfail(PF_E_HIP, "run: device EKF launch failed");
+          hipMemcpyAsync(exf, ex0, nx * 8, hipMemcpyDeviceToDevice, h->stream) != hipSuccess ||
+          hipMemcpyAsync(ePf, eP0, (size_t)nx * nx * 8, hipMemcpyDeviceToDevice, h->stream) != hipSuccess) {
+        st = lfail(PF_E_HIP, "run: EKF input upload failed");
         break;
       }
-    }
-    // the flow tables depend on (P_k, z_k) only, not on the particles: build all T at once
-    const size_t tsz = TLayHost(nx, nz, h->L);
-    if (h->shared) {
-      if (hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
-        st = lfail(PF_E_HIP, "hipMalloc of the run's flow tables failed");
+      hipEvent_t up;
+      if (hipEventCreateWithFlags(&up, hipEventDisableTiming) != hipSuccess || hipEventRecord(up, h->stream) != hipSuccess ||
+          hipStreamWaitEvent(h->side, up, 0) != hipSuccess) {
+        st = lfail(PF_E_HIP, "run: event setup failed");
         break;
       }
-      for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += 65535) {  // grid.y <= 65535 steps per launch
-        FlowParams fp = flow_params(h, dP + c0 * nx * nx, dZ + c0 * nz, nullptr, noise, nullptr, nullptr);
-        fp.pk_stride = (int64_t)nx * nx;
-        fp.z_stride = nz;
-        fp.table_stride = (int64_t)tsz;
-        if (h->ops->setup(fp, dTab + c0 * tsz, h->L, (int)std::min<int64_t>(65535, T - c0), h->stream) != hipSuccess)
+      evs.push_back(up);
+      for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += CH) {
+        const int64_t n = std::min(CH, T - c0);
+        hipEvent_t ev;
+        if (h->ops->ekf(h->Pm, exf, ePf, eQ, eR, dZ + c0 * nz, n, dP + c0 * nx * nx, exf, ePf, h->side) != hipSuccess ||
+            !tables(c0, n, h->side) || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(ev, h->side) != hipSuccess) {
+          st = lfail(PF_E_HIP, "run: device EKF / flow-table launch failed");
+          break;
+        }
+        evs.push_back(ev);
+      }
+    } else {
+      for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += 65535)  // grid.y <= 65535 steps per launch
+        if (!tables(c0, std::min<int64_t>(65535, T - c0), h->stream))
           st = lfail(PF_E_HIP, "run: batched flow-table launch failed");
-      }
-      if (st != PF_OK) break;
     }
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
+      if (ekf && t % CH == 0 && hipStreamWaitEvent(h->stream, evs[1 + t / CH], 0) != hipSuccess) {
+        st = lfail(PF_E_HIP, "run: stream wait failed");
+        break;
+      }
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
                         df + t, dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
     }
+    if (ekf) (void)hipStreamSynchronize(h->side);
+    for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     if (st != PF_OK) break;
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
       st = lfail(PF_E_HIP, "run: stream synchronisation failed");
