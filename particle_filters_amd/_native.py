@@ -1,5 +1,5 @@
-"""ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h`` and
-``include/pf_ledh.h``).
+"""ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h``,
+``include/pf_ledh.h`` and ``include/pf_edh.h``).
 
 The library is built in-tree by ``__graft_entry__.build()`` (``make -C
 particle_filters_amd/csrc``).  There is no fallback: if the library is missing
@@ -38,6 +38,8 @@ PF_NOISE_HOST = 1
 PF_NOISE_DEVICE = 2
 PF_LEDH_FLOW_AUTO = 0
 PF_LEDH_FLOW_PER_PARTICLE = 1
+PF_EDH_RK4 = 0
+PF_EDH_EULER = 1
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -59,6 +61,11 @@ class Opts(C.Structure):
 class LedhOpts(C.Structure):
     _fields_ = [("n_particles", C.c_int64), ("n_lambda", C.c_int32), ("resample_ess_ratio", C.c_double),
                 ("seed", C.c_uint64), ("device", C.c_int32), ("flow_mode", C.c_int32)]
+
+
+class EdhOpts(C.Structure):
+    _fields_ = [("n_particles", C.c_int64), ("n_lambda", C.c_int32), ("resample_ess_ratio", C.c_double),
+                ("seed", C.c_uint64), ("device", C.c_int32), ("integrator", C.c_int32)]
 
 
 class LedhInfo(C.Structure):
@@ -113,6 +120,11 @@ SIGNATURES = {
     "pf_ledh_stream": (_vp, [_vp]),
     "pf_ledh_synchronize": (C.c_int32, [_vp]),
     "pf_ledh_shared_path": (C.c_int32, [_vp]),
+    # include/pf_edh.h
+    "pf_edh_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(EdhOpts), C.POINTER(_vp)]),
+    "pf_edh_step": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, C.c_int32, _dp, C.POINTER(LedhInfo), _dp]),
+    "pf_edh_run": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp, C.POINTER(C.c_uint8)]),
+    "pf_edh_is_edh": (C.c_int32, [_vp]),
 }
 
 _lib = None

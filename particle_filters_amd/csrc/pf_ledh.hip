@@ -13,6 +13,7 @@
 #include "../../include/pf_ledh.h"
 #include "pf_ledh_ekf.h"
 #include "pf_ledh_kernels.h"
+#include "pf_edh_kernels.h"
 
 namespace pf {
 // the engine's thread-local error message (pf_last_error, pf_engine.hip)
@@ -23,10 +24,11 @@ static pf_status lfail(pf_status code, const std::string& msg) {
   return code;
 }
 
-// size (doubles) of the shared-path flow table, TLay<nx, nz>::size(L)
+// size (doubles) of the shared-path flow table, TLay<nx, nz>::size(L); its aff block also holds
+// the EDH general map (ELay: nx*nx + nx)
 static size_t TLayHost(int nx, int nz, int L) {
   return (size_t)(nx + nz) + (size_t)L * (size_t)(nx * nz + nz * nz + nx + nz + 1) +
-         (size_t)(nx + nx * nz + nz + nz * nz + 1);
+         std::max((size_t)(nx + nx * nz + nz + nz * nz + 1), (size_t)(nx * nx + nx));
 }
 #define LCHK(expr)                                                                          \
   do {                                                                                      \
@@ -46,7 +48,10 @@ struct LOps {
                      uint32_t, hipStream_t);
   void (*prepare)();
   hipError_t (*ekf)(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
-                    const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, hipStream_t);
+                    const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, double* Xp, hipStream_t);
+  // EDH (pf_edh_kernels.h): composed flow maps of n_steps time steps; the particle kernel (nonlinear h)
+  hipError_t (*edh_setup)(const FlowParams&, double*, int, hipStream_t);
+  hipError_t (*flow_edh)(const FlowParams&, hipStream_t);
 };
 
 template <int NX, int NZ, int TK, int OK>
@@ -112,13 +117,29 @@ struct LL {
     return hipGetLastError();
   }
   static hipError_t ekf(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
-                        const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, hipStream_t s) {
-    hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(EB), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out);
+                        const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, double* Xp,
+                        hipStream_t s) {
+    hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(EB), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out,
+                       Xp);
     return hipGetLastError();
+  }
+  static hipError_t edh_setup(const FlowParams& p, double* table, int n_steps, hipStream_t s) {
+    hipLaunchKernelGGL((k_edh_setup<NX, NZ, TK, OK>), dim3(n_steps), dim3(SB), 0, s, p, table);
+    return hipGetLastError();
+  }
+  static hipError_t flow_edh(const FlowParams& p, hipStream_t s) {
+    if constexpr (OK == PF_OBS_LINEAR) {
+      return flow_shared(p, s);  // eta_L = eta0 + d0 + D (H eta0): the LEDH affine kernel, theta = 0
+    } else {
+      hipLaunchKernelGGL((k_flow_edh<NX, NZ, TK, OK>), dim3((unsigned)((p.N + TB - 1) / TB)), dim3(TB), 0, s, p);
+      return hipGetLastError();
+    }
   }
   static LOps make() {
     LOps o;
     o.ekf = &ekf;
+    o.edh_setup = &edh_setup;
+    o.flow_edh = &flow_edh;
     o.nx = NX; o.nz = NZ; o.tk = TK; o.ok = OK;
     o.psize = Lay<NX, NZ>::SIZE;
     o.setup = &setup;
@@ -213,6 +234,8 @@ struct pf_ledh_handle {
   uint64_t seed = 0;
   int device = 0;
   bool shared = false;
+  int algo = 0;   // 0 LEDH, 1 EDH (pf_edh_create)
+  int integ = 0;  // EDH integrator (PF_EDH_RK4 / PF_EDH_EULER)
   int q_diag = 0, r_diag = 0;
   uint32_t epoch = 1;
   bool initialized = false;
@@ -225,6 +248,7 @@ struct pf_ledh_handle {
   double *tmax = nullptr, *tsum = nullptr, *trec = nullptr, *cdf = nullptr, *stat = nullptr, *mean = nullptr;
   double* mean_prev = nullptr;  // shift of the one-pass moments (ping-pong with mean)
   double *cpart = nullptr, *Pm = nullptr, *Pk = nullptr, *z = nullptr, *u = nullptr, *vbuf = nullptr;
+  double* xbar = nullptr;  // EDH: tracker past mean of the current step
   double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
 };
 
@@ -255,6 +279,9 @@ FlowParams flow_params(pf_ledh_handle* h, const double* Pk, const double* z, con
   p.epoch = h->epoch;
   p.q_diag = h->q_diag;
   p.r_diag = h->r_diag;
+  p.xbar = nullptr;
+  p.xbar_stride = p.u_stride = 0;
+  p.integ = h->integ;
   return p;
 }
 
@@ -290,11 +317,19 @@ WParams w_params(pf_ledh_handle* h) {
 // flow + weights + decision of one step (ledh.py:104-203), all enqueued on h->stream
 pf_status enqueue_flow(pf_ledh_handle* h, const double* Pk, const double* z, const double* u, int noise,
                        const double* v, double* diagS, double* o_ess, int32_t* o_flag,
-                       const double* pre_table = nullptr) {
+                       const double* pre_table = nullptr, const double* xbar = nullptr) {
   const uint32_t ep_noise = ++h->epoch;
   FlowParams fp = flow_params(h, Pk, z, u, noise, v, diagS);
   fp.epoch = ep_noise;
-  if (h->shared) {
+  if (h->algo == 1) {  // EDH: one composed affine map per step (pf_edh_kernels.h)
+    if (pre_table) {
+      fp.table = pre_table;
+    } else {
+      fp.xbar = xbar;
+      LCHK(h->ops->edh_setup(fp, h->table, 1, h->stream));
+    }
+    LCHK(h->ops->flow_edh(fp, h->stream));
+  } else if (h->shared) {
     if (pre_table) fp.table = pre_table;  // built for the whole run up front (pf_ledh_run)
     else LCHK(h->ops->setup(fp, h->table, h->L, 1, h->stream));
     LCHK(h->ops->flow_shared(fp, h->stream));
@@ -345,7 +380,11 @@ int32_t pf_ledh_model_supported(int32_t nx, int32_t nz, int32_t tk, int32_t ok) 
   return find_lops(nx, nz, tk, ok) != nullptr;
 }
 
-pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_handle** out) {
+}  // extern "C"
+
+// LEDHFlowPF.__init__ (ledh.py:63-81) / EDHFlowPF.__init__ (edh.py:138-171): algo 0 LEDH, 1 EDH
+static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int algo, int integ,
+                             pf_ledh_handle** out) {
   if (!m || !o || !out) return lfail(PF_E_ARG, "null argument");
   *out = nullptr;
   if (o->n_particles <= 0) return lfail(PF_E_ARG, "n_particles must be positive");
@@ -400,7 +439,9 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
   h->N = o->n_particles;
   h->Npad = (h->N + 3) / 4 * 4;
   h->L = std::max(1, (int)o->n_lambda);                   // ledh.py:132
-  if ((size_t)h->L * (size_t)(nx * nz + nz * nz + nx + nz + 1) * 8 > 120 * 1024) {
+  h->algo = algo;
+  h->integ = integ;
+  if (algo == 0 && (size_t)h->L * (size_t)(nx * nz + nz * nz + nx + nz + 1) * 8 > 120 * 1024) {
     delete h;
     return lfail(PF_E_ARG, "n_lambda_steps too large for the staged flow table of this model");
   }
@@ -445,16 +486,39 @@ pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_
   if (hipMemcpy(h->Pm, P.data(), P.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->d_lams, h->lams.data(), h->lams.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
     return bail("upload");
+  if (algo == 1 && hipMalloc((void**)&h->xbar, (size_t)nx * 8) != hipSuccess) return bail("xbar");
   *out = h;
   return PF_OK;
 }
+
+extern "C" {
+
+pf_status pf_ledh_create(const pf_model_desc* m, const pf_ledh_opts* o, pf_ledh_handle** out) {
+  return create_impl(m, o, 0, 0, out);
+}
+
+pf_status pf_edh_create(const pf_model_desc* m, const pf_edh_opts* o, pf_ledh_handle** out) {
+  if (!o) return lfail(PF_E_ARG, "null argument");
+  if (o->integrator != PF_EDH_RK4 && o->integrator != PF_EDH_EULER) return lfail(PF_E_ARG, "bad EDH integrator");
+  pf_ledh_opts lo;
+  lo.n_particles = o->n_particles;
+  lo.n_lambda = o->n_lambda;
+  lo.resample_ess_ratio = o->resample_ess_ratio;
+  lo.seed = o->seed;
+  lo.device = o->device;
+  lo.flow_mode = PF_LEDH_FLOW_AUTO;
+  return create_impl(m, &lo, 1, o->integrator, out);
+}
+
+int32_t pf_edh_is_edh(pf_ledh_handle* h) { return (h && h->algo == 1) ? 1 : 0; }
 
 void pf_ledh_destroy(pf_ledh_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
-                    h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc})
+                    h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
+                    h->xbar})
     if (p) (void)hipFree(p);
   if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->side) (void)hipStreamDestroy(h->side);
@@ -496,8 +560,26 @@ pf_status pf_ledh_init(pf_ledh_handle* h, const double* mean0, const double* cov
   return PF_OK;
 }
 
+static pf_status step_impl(pf_ledh_handle* h, const double* P, const double* xbar, const double* z, const double* u,
+                           int32_t noise, const double* v, pf_ledh_info* info, double* cond_S);
+
 pf_status pf_ledh_step(pf_ledh_handle* h, const double* P, const double* z, const double* u, int32_t noise,
                        const double* v, pf_ledh_info* info, double* cond_S) {
+  if (h && h->algo == 1) return lfail(PF_E_ARG, "EDH handle: use pf_edh_step (it needs the tracker's past mean)");
+  return step_impl(h, P, nullptr, z, u, noise, v, info, cond_S);
+}
+
+pf_status pf_edh_step(pf_ledh_handle* h, const double* P, const double* xbar, const double* z, const double* u,
+                      int32_t noise, const double* v, pf_ledh_info* info, double* cond_S) {
+  if (h && h->algo != 1) return lfail(PF_E_ARG, "pf_edh_step needs a handle from pf_edh_create");
+  if (!xbar) return lfail(PF_E_ARG, "null argument");
+  return step_impl(h, P, xbar, z, u, noise, v, info, cond_S);
+}
+
+}  // extern "C"
+
+static pf_status step_impl(pf_ledh_handle* h, const double* P, const double* xbar, const double* z, const double* u,
+                           int32_t noise, const double* v, pf_ledh_info* info, double* cond_S) {
   if (!h || !P || !z) return lfail(PF_E_ARG, "null argument");
   if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (noise == PF_NOISE_HOST && !v) return lfail(PF_E_ARG, "PF_NOISE_HOST needs v");
@@ -506,12 +588,13 @@ pf_status pf_ledh_step(pf_ledh_handle* h, const double* P, const double* z, cons
   if (sym_upload(h, P, h->Pk) != PF_OK) return PF_E_HIP;
   LCHK(hipMemcpyAsync(h->z, z, h->nz * 8, hipMemcpyHostToDevice, h->stream));
   if (u) LCHK(hipMemcpyAsync(h->u, u, h->nx * 8, hipMemcpyHostToDevice, h->stream));
+  if (xbar) LCHK(hipMemcpyAsync(h->xbar, xbar, h->nx * 8, hipMemcpyHostToDevice, h->stream));
   if (noise == PF_NOISE_HOST) {
     if (!h->vbuf) LCHK(hipMalloc((void**)&h->vbuf, (size_t)h->N * h->nx * 8));
     LCHK(hipMemcpyAsync(h->vbuf, v, (size_t)h->N * h->nx * 8, hipMemcpyHostToDevice, h->stream));
   }
   pf_status st = enqueue_flow(h, h->Pk, h->z, u ? h->u : nullptr, noise, noise == PF_NOISE_HOST ? h->vbuf : nullptr,
-                              cond_S ? h->diagS : nullptr, nullptr, nullptr);
+                              cond_S ? h->diagS : nullptr, nullptr, nullptr, nullptr, xbar ? h->xbar : nullptr);
   if (st != PF_OK) return st;
   double stat[3];
   LCHK(hipMemcpyAsync(stat, h->stat, 3 * 8, hipMemcpyDeviceToHost, h->stream));
@@ -525,6 +608,8 @@ pf_status pf_ledh_step(pf_ledh_handle* h, const double* P, const double* z, cons
   }
   return PF_OK;
 }
+
+extern "C" {
 
 pf_status pf_ledh_finish(pf_ledh_handle* h, const double* U, double* mean, double* cov) {
   if (!h) return lfail(PF_E_ARG, "null argument");
@@ -599,9 +684,13 @@ struct EkfSpec {
 
 // The T loop (pf_ledh_run / pf_ledh_run_ekf): tracker covariances from the host (Ps) or from the
 // device EKF, all flow tables built up front, then flow -> weights -> resample -> moments per step.
-pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, const double* Z, const double* U, int64_t T,
-                   int32_t noise, double* means, double* covs, double* ess, uint8_t* flags) {
+// EDH handles also take the tracker's past means Xb [T][nx] (host) or get them from the device EKF.
+pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const EkfSpec* ekf, const double* Z,
+                   const double* U, int64_t T, int32_t noise, double* means, double* covs, double* ess,
+                   uint8_t* flags) {
   if (!h || !Z || (!Ps && !ekf)) return lfail(PF_E_ARG, "null argument");
+  const bool edh = h->algo == 1;
+  if (edh && !ekf && !Xb) return lfail(PF_E_ARG, "EDH run needs the tracker's past means");
   if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (noise != PF_NOISE_NONE && noise != PF_NOISE_DEVICE) return lfail(PF_E_ARG, "run: noise must be NONE or DEVICE");
   if (T <= 0) return PF_OK;
@@ -617,9 +706,10 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, cons
   }
   double *dP = nullptr, *dZ = nullptr, *dU = nullptr, *dm = nullptr, *dc = nullptr, *de = nullptr, *dTab = nullptr;
   double* dE = nullptr;  // EKF inputs / outputs: x0 | P0 | Qt | Rt | x_final | P_final
+  double* dX = nullptr;  // EDH: past means [T][nx]
   int32_t* df = nullptr;
   auto cleanup = [&]() {
-    for (double* p : {dP, dZ, dU, dm, dc, de, dTab, dE})
+    for (double* p : {dP, dZ, dU, dm, dc, de, dTab, dE, dX})
       if (p) (void)hipFree(p);
     if (df) (void)hipFree(df);
   };
@@ -630,7 +720,8 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, cons
             hipMalloc((void**)&dm, (size_t)T * nx * 8) == hipSuccess &&
             hipMalloc((void**)&dc, (size_t)T * nx * nx * 8) == hipSuccess &&
             hipMalloc((void**)&de, (size_t)T * 8) == hipSuccess && hipMalloc((void**)&df, (size_t)T * 4) == hipSuccess &&
-            (!ekf || hipMalloc((void**)&dE, ne * 8) == hipSuccess);
+            (!ekf || hipMalloc((void**)&dE, ne * 8) == hipSuccess) &&
+            (!edh || hipMalloc((void**)&dX, (size_t)T * nx * 8) == hipSuccess);
   if (!ok) {
     cleanup();
     return lfail(PF_E_HIP, "hipMalloc of run buffers failed");
@@ -639,23 +730,32 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, cons
   do {
     if ((Ps && hipMemcpyAsync(dP, S.data(), S.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
         hipMemcpyAsync(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-        (U && hipMemcpyAsync(dU, U, (size_t)T * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)) {
+        (U && hipMemcpyAsync(dU, U, (size_t)T * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
+        (edh && !ekf && hipMemcpyAsync(dX, Xb, (size_t)T * nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)) {
       st = lfail(PF_E_HIP, "upload of run inputs failed");
       break;
     }
     double *ex0 = dE, *eP0 = dE + nx, *eQ = eP0 + nx * nx, *eR = eQ + nx * nx, *exf = eR + nz * nz, *ePf = exf + nx;
     const size_t tsz = TLayHost(nx, nz, h->L);
-    if (h->shared && hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
+    const bool tabled = h->shared || edh;
+    if (tabled && hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
       st = lfail(PF_E_HIP, "hipMalloc of the run's flow tables failed");
       break;
     }
     // flow tables of steps [c0, c0 + n) (they depend on (P_k, z_k) only, not on the particles)
     auto tables = [&](int64_t c0, int64_t n, hipStream_t s) -> bool {
-      if (!h->shared) return true;
+      if (!tabled) return true;
       FlowParams fp = flow_params(h, dP + c0 * nx * nx, dZ + c0 * nz, nullptr, noise, nullptr, nullptr);
       fp.pk_stride = (int64_t)nx * nx;
       fp.z_stride = nz;
       fp.table_stride = (int64_t)tsz;
+      if (edh) {
+        fp.xbar = dX + c0 * nx;
+        fp.xbar_stride = nx;
+        fp.u = dU ? dU + c0 * nx : nullptr;
+        fp.u_stride = nx;
+        return h->ops->edh_setup(fp, dTab + c0 * tsz, (int)n, s) == hipSuccess;
+      }
       return h->ops->setup(fp, dTab + c0 * tsz, h->L, (int)n, s) == hipSuccess;
     };
     // Device tracker: the EKF and the tables run on the side stream CH steps at a time, ahead of the
@@ -682,7 +782,8 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const EkfSpec* ekf, cons
       for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += CH) {
         const int64_t n = std::min(CH, T - c0);
         hipEvent_t ev;
-        if (h->ops->ekf(h->Pm, exf, ePf, eQ, eR, dZ + c0 * nz, n, dP + c0 * nx * nx, exf, ePf, h->side) != hipSuccess ||
+        if (h->ops->ekf(h->Pm, exf, ePf, eQ, eR, dZ + c0 * nz, n, dP + c0 * nx * nx, exf, ePf,
+                        edh ? dX + c0 * nx : nullptr, h->side) != hipSuccess ||
             !tables(c0, n, h->side) || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(ev, h->side) != hipSuccess) {
           st = lfail(PF_E_HIP, "run: device EKF / flow-table launch failed");
@@ -736,7 +837,15 @@ extern "C" {
 pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T, int32_t noise,
                       double* means, double* covs, double* ess, uint8_t* flags) {
   if (!Ps) return lfail(PF_E_ARG, "null argument");
-  return run_impl(h, Ps, nullptr, Z, U, T, noise, means, covs, ess, flags);
+  if (h && h->algo == 1) return lfail(PF_E_ARG, "EDH handle: use pf_edh_run (it needs the tracker's past means)");
+  return run_impl(h, Ps, nullptr, nullptr, Z, U, T, noise, means, covs, ess, flags);
+}
+
+pf_status pf_edh_run(pf_ledh_handle* h, const double* Ps, const double* Xbars, const double* Z, const double* U,
+                     int64_t T, int32_t noise, double* means, double* covs, double* ess, uint8_t* flags) {
+  if (!Ps || !Xbars) return lfail(PF_E_ARG, "null argument");
+  if (h && h->algo != 1) return lfail(PF_E_ARG, "pf_edh_run needs a handle from pf_edh_create");
+  return run_impl(h, Ps, Xbars, nullptr, Z, U, T, noise, means, covs, ess, flags);
 }
 
 pf_status pf_ledh_run_ekf(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt, const double* Rt,
@@ -744,7 +853,7 @@ pf_status pf_ledh_run_ekf(pf_ledh_handle* h, const double* x0, const double* P0,
                           double* ess, uint8_t* flags, double* x_final, double* P_final) {
   if (!x0 || !P0 || !Qt || !Rt) return lfail(PF_E_ARG, "null argument");
   EkfSpec e{x0, P0, Qt, Rt, x_final, P_final};
-  return run_impl(h, nullptr, &e, Z, U, T, noise, means, covs, ess, flags);
+  return run_impl(h, nullptr, nullptr, &e, Z, U, T, noise, means, covs, ess, flags);
 }
 
 pf_status pf_ledh_ekf_sequence(pf_ledh_handle* h, const double* x0, const double* P0, const double* Qt,
@@ -767,7 +876,7 @@ pf_status pf_ledh_ekf_sequence(pf_ledh_handle* h, const double* x0, const double
         hipMemcpy(eQ, Qt, (size_t)nx * nx * 8, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(eR, Rt, (size_t)nz * nz * 8, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        h->ops->ekf(h->Pm, ex0, eP0, eQ, eR, dZ, T, dP, exf, ePf, h->stream) != hipSuccess ||
+        h->ops->ekf(h->Pm, ex0, eP0, eQ, eR, dZ, T, dP, exf, ePf, nullptr, h->stream) != hipSuccess ||
         hipStreamSynchronize(h->stream) != hipSuccess ||
         (Ps && hipMemcpy(Ps, dP, (size_t)T * nx * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
         (x_final && hipMemcpy(x_final, exf, nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||

@@ -61,7 +61,8 @@ __device__ __forceinline__ double l96_jv(const double* y, const double* V, int a
 template <int NX, int NZ, int TK, int OK>
 __global__ void __launch_bounds__(EB) k_ekf_seq(const double* __restrict__ Pm, const double* x0, const double* P0,
                                                const double* __restrict__ Qt, const double* __restrict__ Rt,
-                                               const double* Z, int64_t T, double* Ps, double* x_out, double* P_out) {
+                                               const double* Z, int64_t T, double* Ps, double* x_out, double* P_out,
+                                               double* Xp) {
   using L = Lay<NX, NZ>;
   using SM = EkfSmem<NX, NZ>;
   __shared__ double sm[SM::SIZE];
@@ -80,6 +81,8 @@ __global__ void __launch_bounds__(EB) k_ekf_seq(const double* __restrict__ Pm, c
   }
   __syncthreads();
   for (int64_t k = 0; k < T; ++k) {
+    if (Xp)  // the tracker's past mean x_{k-1|k-1} (EDH linearisation start, edh.py:200)
+      for (int d = t; d < NX; d += EB) Xp[k * NX + d] = x[d];
     // ---- predict: x = g(x), G = dg/dx at x (extended_kalman_filter.py:178-192) -------
     if constexpr (TK == PF_TRANS_LINEAR) {
       for (int d = t; d < NX; d += EB) {

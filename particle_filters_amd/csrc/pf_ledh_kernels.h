@@ -111,6 +111,10 @@ struct FlowParams {
   uint64_t seed;
   uint32_t epoch;
   int q_diag, r_diag;
+  // EDH (pf_edh_kernels.h): tracker past means x_{k-1|k-1} [nx] per step, u per step, integrator
+  const double* xbar;
+  int64_t xbar_stride, u_stride;
+  int integ;
 };
 
 // ---------------------------------------------------------------------------
@@ -533,19 +537,13 @@ __device__ __forceinline__ double group_sum(double v) {
   return v;
 }
 
+// eta0 = g(x_{k-1}, u) + v of particle i over a lane group (ledh.py:104-115): gx = g(x) and v
+// (PER components per lane, lane q of the group holds components q*PER ..)
 template <int NX, int NZ, int TK>
-__global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
+__device__ __forceinline__ void group_prior(const FlowParams& p, int64_t i, int q, int base, double* gx, double* v) {
   using L = Lay<NX, NZ>;
-  using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  const int64_t tid = (int64_t)blockIdx.x * TB + threadIdx.x;
-  const int64_t i = tid / GL;
-  if (i >= p.N) return;  // whole groups leave together
-  const int q = (int)(tid % GL);
-  const int lane = threadIdx.x & 63;
-  const int base = lane - q;
   const double* __restrict__ Pm = p.Pm;
-  const double* __restrict__ af = p.table + T::aff(p.L);
   double x[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -553,7 +551,6 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
     x[j] = a < NX ? p.x_in[(int64_t)a * p.Npad + i] : 0.0;
   }
   // ---- g(x_{k-1}, u) ------------------------------------------------------------
-  double gx[PER];
   if constexpr (TK == PF_TRANS_L96) {
     static_assert(NX % GL == 0 && PER >= 2, "L96 lane groups hold >= 2 contiguous components each");
     const double F = Pm[L::EX], dt = Pm[L::EX + 1];
@@ -598,7 +595,6 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
     }
   }
   // ---- process noise v ------------------------------------------------------------
-  double v[PER];
   if (p.noise == PF_NOISE_HOST) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -623,6 +619,54 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) v[j] = 0.0;
   }
+}
+
+// log N(eta; g(x), Q) - log N(eta0; g(x), Q) up to the cancelling constant (ledh.py:186-190),
+// dd = eta - g(x), v = eta0 - g(x); summed over the lane group
+template <int NX, int NZ>
+__device__ __forceinline__ double group_trans_part(const FlowParams& p, int q, int base, const double* dd,
+                                                   const double* v) {
+  using L = Lay<NX, NZ>;
+  constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  const double* __restrict__ Pm = p.Pm;
+  double part = 0.0;
+  if (p.q_diag) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int a = q * PER + j;
+      if (a < NX) {
+        const double qi = Pm[L::QI + a * NX + a];
+        part += (-0.5 * (dd[j] * (qi * dd[j]))) - (-0.5 * (v[j] * (qi * v[j])));
+      }
+    }
+  } else {
+    double ta[PER], tb[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) ta[j] = tb[j] = 0.0;
+    group_rows<NX>(dd, Pm + L::QI, q, base, ta, false);
+    group_rows<NX>(v, Pm + L::QI, q, base, tb, false);
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (q * PER + j < NX) part += (-0.5 * (dd[j] * ta[j])) - (-0.5 * (v[j] * tb[j]));
+  }
+  return group_sum<GL>(part);
+}
+
+template <int NX, int NZ, int TK>
+__global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
+  using L = Lay<NX, NZ>;
+  using T = TLay<NX, NZ>;
+  constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  const int64_t tid = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const int64_t i = tid / GL;
+  if (i >= p.N) return;  // whole groups leave together
+  const int q = (int)(tid % GL);
+  const int lane = threadIdx.x & 63;
+  const int base = lane - q;
+  const double* __restrict__ Pm = p.Pm;
+  const double* __restrict__ af = p.table + T::aff(p.L);
+  double gx[PER], v[PER];
+  group_prior<NX, NZ, TK>(p, i, q, base, gx, v);
   // ---- eta0, y0 = H eta0 (group all-reduce), the composed flow ----------------------
   double e0[PER];
 #pragma unroll
@@ -653,27 +697,7 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
     }
   }
   // ---- log weight (ledh.py:186-190) -----------------------------------------------
-  double part = 0.0;
-  if (p.q_diag) {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int a = q * PER + j;
-      if (a < NX) {
-        const double qi = Pm[L::QI + a * NX + a];
-        part += (-0.5 * (dd[j] * (qi * dd[j]))) - (-0.5 * (v[j] * (qi * v[j])));
-      }
-    }
-  } else {
-    double ta[PER], tb[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) ta[j] = tb[j] = 0.0;
-    group_rows<NX>(dd, Pm + L::QI, q, base, ta, false);
-    group_rows<NX>(v, Pm + L::QI, q, base, tb, false);
-#pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if (q * PER + j < NX) part += (-0.5 * (dd[j] * ta[j])) - (-0.5 * (v[j] * tb[j]));
-  }
-  part = group_sum<GL>(part);
+  const double part = group_trans_part<NX, NZ>(p, q, base, dd, v);
   if (q == 0) {
     double ez[NZ];
 #pragma unroll
