@@ -1,5 +1,5 @@
 """ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h``,
-``include/pf_ledh.h`` and ``include/pf_edh.h``).
+``include/pf_ledh.h``, ``include/pf_edh.h`` and ``include/pf_diag.h``).
 
 The library is built in-tree by ``__graft_entry__.build()`` (``make -C
 particle_filters_amd/csrc``).  There is no fallback: if the library is missing
@@ -68,6 +68,11 @@ class EdhOpts(C.Structure):
                 ("seed", C.c_uint64), ("device", C.c_int32), ("integrator", C.c_int32)]
 
 
+class Diagnostics(C.Structure):
+    _fields_ = [("ess", C.c_double), ("entropy", C.c_double), ("entropy_raw", C.c_double), ("gini", C.c_double),
+                ("max_weight", C.c_double), ("posterior_spread", C.c_double), ("n_unique", C.c_int64)]
+
+
 class LedhInfo(C.Structure):
     _fields_ = [("ess", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
 
@@ -125,6 +130,11 @@ SIGNATURES = {
     "pf_edh_step": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, C.c_int32, _dp, C.POINTER(LedhInfo), _dp]),
     "pf_edh_run": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp, C.POINTER(C.c_uint8)]),
     "pf_edh_is_edh": (C.c_int32, [_vp]),
+    # include/pf_diag.h
+    "pf_diagnostics_host": (C.c_int32, [C.c_int32, _dp, _dp, C.c_int64, C.c_int32, C.c_double, _dp,
+                                        C.POINTER(Diagnostics)]),
+    "pf_state_diagnostics": (C.c_int32, [_vp, C.c_double, C.POINTER(Diagnostics)]),
+    "pf_ledh_diagnostics": (C.c_int32, [_vp, C.c_double, C.POINTER(Diagnostics)]),
 }
 
 _lib = None

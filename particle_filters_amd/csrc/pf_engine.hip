@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/pf_engine.h"
+#include "pf_diag.h"
 #include "pf_ops.h"
 #include "pf_resample_w.h"
 
@@ -904,6 +905,46 @@ pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
       }
       if (log_weights) log_weights[o] = l;
     }
+  }
+  return PF_OK;
+}
+
+// diag:61-91 on the device-resident state of every replicate (include/pf_diag.h)
+pf_status pf_state_diagnostics(pf_handle* h, double tol, pf_diagnostics* out) {
+  if (!h || !out) return fail(PF_E_ARG, "null argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->pending) {
+    pf_status st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  StepParams f = base_params(h);
+  const OutSlots o = out_slots(h);
+  set_outputs(f, o, false);
+  f.out_step = 0;
+  pf_status st = launch_finalize(h, f);
+  if (st) return st;
+  std::vector<double> lse(h->R), uni(h->R);
+  HIPCHK(hipMemcpyAsync(lse.data(), o.lse, h->R * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  for (int r = 0; r < h->R; ++r)
+    HIPCHK(hipMemcpyAsync(&uni[r], h->rec[h->crec] + (size_t)r * h->G * h->ops->rec_size + 3 * (size_t)h->G,
+                          sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int r = 0; r < h->R; ++r) {
+    diag::DiagSrc s{};
+    s.N = h->N;
+    s.Npad = h->Npad;
+    s.nx = h->nx;
+    s.w = nullptr;
+    s.lw = (const char*)h->lw[h->clw] + (size_t)r * h->Npad * h->esz;
+    s.lse = lse[r];
+    s.uniform = uni[r] != 0.0;
+    s.x = (const char*)h->x[h->cx] + (size_t)r * h->nx * h->Npad * h->esz;
+    s.real_is_double = h->esz == 8;
+    s.tol = tol;
+    s.spread = NAN;
+    st = diag::compute(s, h->stream, out + r);
+    if (st) return st;
   }
   return PF_OK;
 }

@@ -13,6 +13,7 @@
 #include "../../include/pf_ledh.h"
 #include "pf_ledh_ekf.h"
 #include "pf_ledh_kernels.h"
+#include "pf_diag.h"
 #include "pf_edh_kernels.h"
 
 namespace pf {
@@ -656,6 +657,23 @@ pf_status pf_ledh_get_weights(pf_ledh_handle* h, double* weights) {
   LCHK(hipStreamSynchronize(h->stream));
   LCHK(hipMemcpy(weights, h->w, (size_t)h->N * 8, hipMemcpyDeviceToHost));
   return PF_OK;
+}
+
+// diag:61-91 on the device-resident state (include/pf_diag.h)
+pf_status pf_ledh_diagnostics(pf_ledh_handle* h, double tol, pf_diagnostics* out) {
+  if (!h || !out) return lfail(PF_E_ARG, "null argument");
+  if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  LCHK(hipSetDevice(h->device));
+  pf::diag::DiagSrc s{};
+  s.N = h->N;
+  s.Npad = h->Npad;
+  s.nx = h->nx;
+  s.w = h->w;
+  s.x = h->x;
+  s.real_is_double = 1;
+  s.tol = tol;
+  s.spread = NAN;
+  return pf::diag::compute(s, h->stream, out);
 }
 
 pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const double* weights) {
