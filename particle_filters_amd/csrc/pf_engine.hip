@@ -113,6 +113,8 @@ struct pf_handle {
   uint32_t ep_res = 0;        // epoch reserved by the last update for its resample
   bool chol_q_ok = true;
   int lq_local = 0, lj_local = 0;  // chol(Q) / 0.001 chol(Q) block-diagonal in nx/4 blocks (k_step_grp)
+  int sys_cdf = 0;  // systematic ancestors from the materialised CDF (k_cdf) instead of per-tile scans
+  bool needs_cdf() const { return method == 1 || sys_cdf; }
   std::vector<double> Pd;     // params (double)
   // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
   unsigned long long* rsync = nullptr;
@@ -180,6 +182,7 @@ StepParams base_params(pf_handle* h) {
   p.rep_base = h->rep_base;
   p.lq_local = h->lq_local;
   p.lj_local = h->lj_local;
+  p.sys_cdf = h->sys_cdf;
   p.out_step = -1;
   p.out_post_step = -1;
   p.z_rs = h->nz;
@@ -278,7 +281,7 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
   p.cdf = h->cdf;
   p.allow_gather = 1;
   p.ep_resample = h->ep_res;
-  if (h->method == 1) {
+  if (h->needs_cdf()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -471,6 +474,10 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   h->Npad = (o->n_particles + 3) / 4 * 4;
   h->R = o->n_replicates;
   h->method = o->resample_method == PF_RESAMPLE_SYSTEMATIC ? 0 : 1;
+  {  // large-state kernels: systematic ancestors by one binary search in the k_cdf-materialised CDF
+    const char* env = std::getenv("PF_SYS_CDF");
+    h->sys_cdf = (h->method == 0 && ops->grp && !(env && env[0] == '0')) ? 1 : 0;
+  }
   h->thresh = o->resample_thresh;
   h->regularize = o->regularize != 0;
   h->seed = o->seed;
@@ -512,7 +519,7 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
     (void)hipMemset(h->x[k], 0, xbytes);
     (void)hipMemset(h->lw[k], 0, lwbytes);
   }
-  if (h->method == 1 && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
+  if (h->needs_cdf() && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of cdf failed"));
   if (hipMalloc(&h->P, P.size() * h->esz) != hipSuccess || hipMalloc(&h->d_z, (size_t)h->R * nz * h->esz) != hipSuccess ||
       hipMalloc(&h->d_u, (size_t)h->R * nx * h->esz) != hipSuccess ||
@@ -600,7 +607,7 @@ pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
   }
   // a resample decided but not yet applied is fused into this launch
   const bool gather = h->pending;
-  if (gather && h->method == 1) {
+  if (gather && h->needs_cdf()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -740,7 +747,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     p.ep_resample = prev_res;
     p.out_step = s >= 1 ? s - 1 : -1;
     p.out_post_step = s >= 2 ? s - 2 : -1;
-    if (gather_possible && h->method == 1) {
+    if (gather_possible && h->needs_cdf()) {
       pf_status st = launch_cdf(h, p);
       if (st) return st;
     }
@@ -759,7 +766,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   p.ep_resample = prev_res;
   p.out_step = T - 1;
   p.out_post_step = T >= 2 ? T - 2 : -1;
-  if (h->method == 1) {
+  if (h->needs_cdf()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -1118,7 +1125,7 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
     p.ep_resample = prev_res;
     p.out_step = s >= 1 ? s - 1 : -1;
     p.out_post_step = s >= 2 ? s - 2 : -1;
-    if (gather_possible && h->method == 1) st = launch_cdf(h, p);
+    if (gather_possible && h->needs_cdf()) st = launch_cdf(h, p);
     if (!st) {
       (void)hipEventRecord(ev[s], h->stream);
       st = launch_step(h, p, true, true, true);
@@ -1136,7 +1143,7 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
     q.allow_gather = 1;
     q.ep_resample = prev_res;
     q.cdf = h->cdf;
-    if (h->method == 1) st = launch_cdf(h, q);
+    if (h->needs_cdf()) st = launch_cdf(h, q);
     if (!st) st = launch_step(h, q, true, false, true);
   }
   (void)hipStreamSynchronize(h->stream);

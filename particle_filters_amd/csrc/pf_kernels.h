@@ -219,6 +219,7 @@ struct StepParams {
   int force_gather;       // resample regardless of Neff (ParticleFilter._resample after its own test)
   int rep_base;           // global id of replicate 0 of this launch (Philox counter word)
   int lq_local, lj_local; // chol(Q) / jitter factor block-diagonal in the lane blocks of k_step_grp
+  int sys_cdf;            // systematic ancestors searched in the materialised CDF `cdf` (k_step_grp)
 };
 
 struct Head {

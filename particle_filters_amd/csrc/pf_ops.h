@@ -18,6 +18,7 @@ namespace pf {
 struct Ops {
   int nx, nz, tk, ok, prec;
   int rec_size, ch, tile_max, tile_min, psize;
+  int grp;  // the step kernel is k_step_grp (lane groups per particle)
   hipError_t (*step)(const StepParams&, dim3, size_t, hipStream_t);
   hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
   hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
@@ -87,6 +88,7 @@ struct Launch {
     // large states (k_step_grp): one particle per lane group per round -> 256 / GL particles
     o.tile_min = SGrp<NX>::ON ? 256 / SGrp<NX>::GL : BS * StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.psize = ParamLayout<NX, NZ>::SIZE;
+    o.grp = SGrp<NX>::ON ? 1 : 0;
     o.step = &step;
     o.finalize = &finalize;
     o.cdf = &cdf;

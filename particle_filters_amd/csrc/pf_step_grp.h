@@ -383,7 +383,25 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
 
   // ---- (1) ancestors of the tile's slots (lane 0 of each group) ---------------
   if (gather) {
-    if (p.method == 0) {
+    if (p.method == 0 && p.sys_cdf) {
+      // the tile of pos from the prefix Pl, then the slot inside that tile's span of the CDF that
+      // k_cdf materialised (tile_cdf arithmetic: the same ancestors as the per-tile path below)
+      const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
+      const double* C = p.cdf + (int64_t)r * p.N;
+      if (q == 0)
+        for (int c = vt; c < nchunks; c += VB) {
+          const double pos = (U + (double)(o0 + c)) / (double)p.N;
+          const int k = prefix_tile(Pl, p.G, pos);
+          const int64_t s0 = (int64_t)k * p.tile;
+          const int len = (int)min((int64_t)p.tile, p.N - s0);
+          int lo = 0, hi = len;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pos < C[s0 + mid]) hi = mid; else lo = mid + 1;
+          }
+          anc_l[c] = (int)(s0 + (lo < len ? lo : len - 1));
+        }
+    } else if (p.method == 0) {
       const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
       int nextk = p.G;
       if (q == 0)

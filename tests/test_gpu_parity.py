@@ -260,3 +260,32 @@ def test_device_rng_statistics_match_oracle(golden_sv):
     assert np.all(np.abs(rmse_e - rmse_o) < 3e-3)
     np.testing.assert_allclose(r.means[:, :, 0].mean(axis=1), o["means"][:, 0], atol=0.05)
     assert abs(np.mean(r.flags) - np.mean(o["flags"])) < 0.03
+
+
+@pytest.mark.parametrize("workload", ["l96", "mat"])
+def test_global_cdf_systematic_is_bitwise_the_tile_scan(workload, golden_l96, golden_mat, monkeypatch):
+    """Large-state kernels find systematic ancestors by a binary search in the k_cdf-materialised
+    CDF (PF_SYS_CDF, default); the per-tile CDF scan it replaced must give identical runs."""
+    if workload == "l96":
+        g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+        Q, R = 0.01 * np.eye(40), np.eye(10)
+        Z = golden_l96["obs"][1:40]
+        m0, c0 = golden_l96["ensemble"][0, 0], 2.0 * np.eye(40)
+        n = 30011
+    else:
+        g, h = M.CVTransition(4, 1.0), M.AcousticObservation(golden_mat["S"], 10.0, 0.1, 4)
+        Q, R = np.kron(np.eye(4), np.diag([1.0, 1.0, 0.01, 0.01])) * 0.1, 0.01 * np.eye(25)
+        Z = golden_mat["Z"][1:30]
+        m0, c0 = golden_mat["X"][0].reshape(-1), np.eye(16)
+        n = 20011
+    runs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("PF_SYS_CDF", flag)
+        b = ParticleFilterBatch(g, h, Q, R, Np=n, n_replicates=2, seed=17, resample_thresh=0.5)
+        b.initialize(m0, c0)
+        runs.append((b.run(Z), b.particles()))
+    (ra, xa), (rb, xb) = runs
+    assert ra.flags.sum() >= 3
+    assert np.array_equal(ra.flags, rb.flags)
+    assert np.array_equal(ra.means, rb.means)
+    assert np.array_equal(xa, xb)
