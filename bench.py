@@ -19,6 +19,7 @@ Workloads (BASELINE.json configs; the default is the headline metric's config):
   mat  config 4: joint 4-target acoustic tracking (nx = 16, nz = 25), N = 1e5,
        8 replicates per GPU (64 over 8 GPUs)
   ledh config 5: LEDH particle flow on L96 d = 40, N = 1e4, 8 lambda steps (fp64)
+  edh  config 5's job with the EDH global flow (EDH_particle_filter.py, RK4) (fp64)
 
 Extra JSON fields:
   roofline      dominant kernel.  SV: k_resident<f32, SV> — ONE launch runs all K
@@ -172,7 +173,7 @@ class MAT(Workload):
                 "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
 
 
-WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT, "ledh": None}
+WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT, "ledh": None, "edh": None}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector 157.3 TF of MI355X_MICROARCH.md)
 
 
@@ -189,8 +190,9 @@ def ledh_flops_per_particle(nx, nz, L):
     return rk4 + noise + y0 + L * per_lam + quad
 
 
-def main_ledh(args, world, rank, local):
-    """BASELINE config 5: LEDH particle flow on Lorenz-96 d = 40, N = 1e4, 8 lambda steps."""
+def main_ledh(args, world, rank, local, algo="ledh"):
+    """BASELINE config 5: LEDH particle flow on Lorenz-96 d = 40, N = 1e4, 8 lambda steps
+    (algo="edh": the same job with the EDH global flow of EDH_particle_filter.py, RK4 integrator)."""
     import torch
 
     torch.cuda.set_device(local)
@@ -199,7 +201,7 @@ def main_ledh(args, world, rank, local):
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from particle_filters_amd import ledh as LD, models as M, simulators as S, trackers as TR
+    from particle_filters_amd import edh as ED, ledh as LD, models as M, simulators as S, trackers as TR
 
     K = args.steps if args.steps is not None else 200
     W = args.warmup if args.warmup is not None else 20
@@ -213,11 +215,14 @@ def main_ledh(args, world, rank, local):
     def make():
         ekf = TR.ExtendedKalmanFilter(g, h, Q, R, jac_g=g.jacobian, jac_h=h.jacobian)
         tracker = TR.EKFTracker(ekf, TR.EKFState(mean0.copy(), cov0.copy(), 0))
+        args_ = (tracker, g, h, h.jacobian, M.GaussianTransitionDensity(g, Q), M.GaussianLikelihood(h, R), R)
+        if algo == "edh":
+            cfg = ED.EDHConfig(n_particles=Np, n_lambda_steps=L, resample_ess_ratio=0.5, flow_integrator="rk4",
+                               rng=np.random.default_rng(42 + rank))
+            return ED.EDHFlowPF(*args_, cfg, rng_mode="device"), tracker
         cfg = LD.LEDHConfig(n_particles=Np, n_lambda_steps=L, resample_ess_ratio=0.5,
                             rng=np.random.default_rng(42 + rank))
-        pf = LD.LEDHFlowPF(tracker, g, h, h.jacobian, M.GaussianTransitionDensity(g, Q), M.GaussianLikelihood(h, R), R,
-                           cfg, rng_mode="device")
-        return pf, tracker
+        return LD.LEDHFlowPF(*args_, cfg, rng_mode="device"), tracker
 
     Z = sim.observations[1:]
     pf, tracker = make()
@@ -243,12 +248,17 @@ def main_ledh(args, world, rank, local):
     pf2.run(st2, Z[:max(W, 1)])
     h0 = time.perf_counter()
     Ps = np.empty((K, nx, nx))
+    Xb = np.empty((K, nx))
     for t in range(K):
         _, P = tracker2.predict()
         Ps[t] = P
+        Xb[t] = tracker2.get_past_mean()
         tracker2.update(Z[W + t])
     t_tr = time.perf_counter() - h0
-    pf2.run(pf2.state, Z[W:W + K], tracker_covs=Ps)
+    if algo == "edh":
+        pf2.run(pf2.state, Z[W:W + K], tracker_seq=(Ps, Xb))
+    else:
+        pf2.run(pf2.state, Z[W:W + K], tracker_covs=Ps)
     torch.cuda.synchronize()
     t_host_total = time.perf_counter() - h0
     pf2.close()
@@ -258,14 +268,18 @@ def main_ledh(args, world, rank, local):
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            from oracle import ledh_oracle as LO
+            from oracle import edh_oracle as EO, ledh_oracle as LO
 
             om = LO.lorenz96(40)
             steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", "1"))
             n_cpu = 1000
             tr = LO.make_ekf_tracker(om, mean0, cov0)
-            opf = LO.LEDHOracle(tr, om, n_particles=n_cpu, n_lambda_steps=L, resample_ess_ratio=0.5,
-                                rng=np.random.default_rng(1), vectorized=False)
+            if algo == "edh":
+                opf = EO.EDHOracle(tr, om, n_particles=n_cpu, n_lambda_steps=L, resample_ess_ratio=0.5,
+                                   rng=np.random.default_rng(1), vectorized=False)
+            else:
+                opf = LO.LEDHOracle(tr, om, n_particles=n_cpu, n_lambda_steps=L, resample_ess_ratio=0.5,
+                                    rng=np.random.default_rng(1), vectorized=False)
             ost = opf.init_from_gaussian(mean0, cov0)
             sampler = lambda n, d: opf.rng.multivariate_normal(np.zeros(d), om.Q, size=n)  # noqa: E731
             c0 = time.perf_counter()
@@ -273,16 +287,19 @@ def main_ledh(args, world, rank, local):
                 ost = opf.step(ost, Z[t], process_noise_sampler=sampler)
             cdt = time.perf_counter() - c0
             cpu = {"value": n_cpu * steps / cdt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                   "sample": f"LEDH L96 d=40, N={n_cpu}, L={L}, {steps} step(s), faithful per-particle restatement "
-                             f"(oracle/ledh_oracle.py, bit-identical to the reference LEDHFlowPF), {cdt:.1f} s",
+                   "sample": f"{algo.upper()} L96 d=40, N={n_cpu}, L={L}, {steps} step(s), faithful per-particle "
+                             f"restatement (oracle/{algo}_oracle.py, bit-identical to the reference "
+                             f"{algo.upper()}FlowPF), {cdt:.1f} s",
                    "cores_on_host": os.cpu_count()}
         line = {
-            "metric": "particle-steps/sec (N×T/s), LEDH flow filter L96 d=40",
+            "metric": f"particle-steps/sec (N×T/s), {algo.upper()} flow filter L96 d=40",
             "value": Np * K * world / elapsed, "unit": "particle-steps/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": elapsed * 1e3 / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)",
-            "config": {"workload": "LEDH particle-flow PF (BASELINE config 5): L96 d=40, N=1e4 particles, 8 lambda "
+            "config": {"workload": ("LEDH particle-flow PF (BASELINE config 5)" if algo == "ledh" else
+                                    "EDH particle-flow PF (config 5's job with the global EDH flow, RK4)") +
+                                   ": L96 d=40, N=1e4 particles, 8 lambda "
                                    "steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
                                    "(analytic RK4 Jacobian), Philox process noise",
                        "n_particles": Np, "n_lambda": L, "shared_jacobian_path": pf.shared_jacobian_path,
@@ -292,8 +309,9 @@ def main_ledh(args, world, rank, local):
                                      "note": "EKF stepped on the host in NumPy, covariances uploaded, same device loop"},
             "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "whole LEDH job: k_ekf_seq + k_setup/k_compose + per step k_flow_affine, "
-                                   "k_weights_small, k_gather, k_mom_part, k_mom_final",
+                         "kernel": ("whole LEDH job: k_ekf_seq + k_setup/k_compose" if algo == "ledh" else
+                                    "whole EDH job: k_ekf_seq + k_edh_setup") +
+                                   " + per step k_flow_affine, k_weights_small, k_gather, k_mom_part, k_mom_final",
                          "flops_per_particle_step": ledh_flops_per_particle(nx, nz, L)},
             "cpu_baseline": cpu,
         }
@@ -329,7 +347,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    if args.workload == "ledh":
+    if args.workload in ("ledh", "edh"):
         return main_ledh(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
                          int(os.environ.get("LOCAL_RANK", "0")))
     wl = WORKLOADS[args.workload]()
