@@ -1,5 +1,5 @@
 """ctypes binding of ``libpf_hip.so`` (the C ABI declared in ``include/pf_engine.h``,
-``include/pf_ledh.h``, ``include/pf_edh.h`` and ``include/pf_diag.h``).
+``include/pf_ledh.h``, ``include/pf_edh.h``, ``include/pf_diag.h`` and ``include/pf_shard.h``).
 
 The library is built in-tree by ``__graft_entry__.build()`` (``make -C
 particle_filters_amd/csrc``).  There is no fallback: if the library is missing
@@ -73,6 +73,10 @@ class Diagnostics(C.Structure):
                 ("max_weight", C.c_double), ("posterior_spread", C.c_double), ("n_unique", C.c_int64)]
 
 
+class ShardStats(C.Structure):
+    _fields_ = [("lse", C.c_double), ("neff", C.c_double), ("U", C.c_double)]
+
+
 class LedhInfo(C.Structure):
     _fields_ = [("ess", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
 
@@ -135,6 +139,11 @@ SIGNATURES = {
                                         C.POINTER(Diagnostics)]),
     "pf_state_diagnostics": (C.c_int32, [_vp, C.c_double, C.POINTER(Diagnostics)]),
     "pf_ledh_diagnostics": (C.c_int32, [_vp, C.c_double, C.POINTER(Diagnostics)]),
+    # include/pf_shard.h
+    "pf_shard_configure": (C.c_int32, [_vp, C.c_int64, C.c_int32]),
+    "pf_shard_update": (C.c_int32, [_vp, _dp, C.c_double, C.POINTER(ShardStats), _dp, _dp]),
+    "pf_shard_offspring": (C.c_int32, [_vp, C.c_double, C.c_double, C.c_double, C.c_int64, C.c_int64, _vp]),
+    "pf_shard_adopt": (C.c_int32, [_vp, _vp, _dp, _dp]),
 }
 
 _lib = None

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/pf_engine.h"
+#include "../../include/pf_shard.h"
 #include "pf_diag.h"
 #include "pf_ops.h"
 #include "pf_resample_w.h"
@@ -114,7 +115,11 @@ struct pf_handle {
   bool chol_q_ok = true;
   int lq_local = 0, lj_local = 0;  // chol(Q) / 0.001 chol(Q) block-diagonal in nx/4 blocks (k_step_grp)
   int sys_cdf = 0;  // systematic ancestors from the materialised CDF (k_cdf) instead of per-tile scans
-  bool needs_cdf() const { return method == 1 || sys_cdf; }
+  // within-filter sharding (pf_shard.h): global index of particle 0, filter size, CDF epoch
+  bool sharded = false;
+  int64_t pbase = 0, n_total = 0;
+  uint32_t shard_cdf_ep = 0;
+  bool needs_cdf() const { return method == 1 || sys_cdf || sharded; }
   std::vector<double> Pd;     // params (double)
   // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
   unsigned long long* rsync = nullptr;
@@ -183,6 +188,7 @@ StepParams base_params(pf_handle* h) {
   p.lq_local = h->lq_local;
   p.lj_local = h->lj_local;
   p.sys_cdf = h->sys_cdf;
+  p.pbase = h->pbase;
   p.out_step = -1;
   p.out_post_step = -1;
   p.z_rs = h->nz;
@@ -311,7 +317,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   *used = false;
   const char* env = std::getenv("PF_RESIDENT");
   if (env && std::atoi(env) == 0) return PF_OK;
-  if (!h->ops->resident || h->method != 0 || !(h->tile == 1024 || h->N <= 1024) || T <= 0) return PF_OK;
+  if (!h->ops->resident || h->method != 0 || h->sharded || !(h->tile == 1024 || h->N <= 1024) || T <= 0) return PF_OK;
   const int G = (int)((h->N + RTILE - 1) / RTILE);
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
   const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
@@ -573,7 +579,7 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   if (!st) {
     const uint32_t ep = h->epoch++;
     hipError_t e = h->ops->init(h->x[h->cx ^ 1], h->rec[h->crec ^ 1], dmean, dL, drep, h->N, h->Npad, h->G, R,
-                                h->seed, ep, h->rep_base, h->stream);
+                                h->seed, ep, h->rep_base, h->pbase, h->stream);
     if (e != hipSuccess) st = fail(PF_E_HIP, std::string("init launch: ") + hipGetErrorString(e));
     h->cx ^= 1;
     h->crec ^= 1;
@@ -913,6 +919,99 @@ pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
       if (log_weights) log_weights[o] = l;
     }
   }
+  return PF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Within-filter sharding (include/pf_shard.h)
+// ---------------------------------------------------------------------------
+pf_status pf_shard_configure(pf_handle* h, int64_t n_total, int32_t rank) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  if (h->R != 1 || h->method != 0) return fail(PF_E_ARG, "sharding needs R = 1 and systematic resampling");
+  if (h->N % 4 != 0 || n_total <= 0 || n_total % h->N != 0 || rank < 0 || (int64_t)rank >= n_total / h->N)
+    return fail(PF_E_ARG, "sharding needs N_loc % 4 == 0, n_total = W * N_loc and 0 <= rank < W");
+  if (n_total / 4 > (int64_t)UINT32_MAX / (h->nx > 0 ? h->nx : 1))
+    return fail(PF_E_ARG, "n_total too large for 32-bit Philox counters");
+  HIPCHK(hipSetDevice(h->device));
+  h->sharded = true;
+  h->n_total = n_total;
+  h->pbase = (int64_t)rank * h->N;
+  if (!h->cdf && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
+    return fail(PF_E_HIP, "hipMalloc of cdf failed");
+  return PF_OK;
+}
+
+pf_status pf_shard_update(pf_handle* h, const double* z, double lse_prev, pf_shard_stats* st, double* mean,
+                          double* cov) {
+  if (!h || !z || !st) return fail(PF_E_ARG, "null argument");
+  if (!h->sharded) return fail(PF_E_ARG, "pf_shard_update needs pf_shard_configure");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  pf_status s = upload_real(h, h->d_z, z, (size_t)h->nz);
+  if (s) return s;
+  StepParams p = base_params(h);
+  p.z = h->d_z;
+  p.do_update = 1;
+  p.use_lse_ext = 1;  // l = (l_prev - lse_global) + loglik (pf.py:254-256 over ALL shards' weights)
+  p.lse_ext = lse_prev;
+  s = launch_step(h, p, false, true, true);
+  if (s) return s;
+  h->ep_res = h->epoch++;  // the resample of this update (U, jitter) uses this epoch on every rank
+  StepParams f = base_params(h);
+  set_outputs(f, out_slots(h), h->nx <= 4);
+  f.out_step = 0;
+  s = launch_finalize(h, f);
+  if (s) return s;
+  std::vector<double> buf(out_doubles(h));
+  HIPCHK(hipMemcpyAsync(buf.data(), h->d_out, buf.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int nx = h->nx;
+  const double* bm = buf.data();
+  const double* bc = bm + nx;
+  const double* bn = bc + (size_t)nx * nx;
+  const double* bl = bn + 1;
+  st->lse = bl[0];
+  st->neff = bn[0];
+  st->U = uniform53(h->seed, 0, (uint32_t)h->rep_base, h->ep_res);
+  if (mean) std::memcpy(mean, bm, (size_t)nx * sizeof(double));
+  if (cov) {
+    if (nx <= 4) std::memcpy(cov, bc, (size_t)nx * nx * sizeof(double));
+    else return pf_moments(h, nullptr, cov);
+  }
+  return PF_OK;
+}
+
+pf_status pf_shard_offspring(pf_handle* h, double U, double lo, double mass, int64_t a, int64_t n, void* out) {
+  if (!h || (n > 0 && !out)) return fail(PF_E_ARG, "null argument");
+  if (!h->sharded) return fail(PF_E_ARG, "pf_shard_offspring needs pf_shard_configure");
+  if (n < 0 || a < 0 || a + n > h->n_total || !(mass > 0.0)) {
+    if (n == 0) return PF_OK;
+    return fail(PF_E_ARG, "pf_shard_offspring: slot range outside the filter or empty segment");
+  }
+  HIPCHK(hipSetDevice(h->device));
+  if (h->shard_cdf_ep != h->ep_res) {  // this update's normalised CDF, once per resample
+    StepParams p = base_params(h);
+    p.allow_gather = 1;
+    p.force_gather = 1;
+    pf_status s = launch_cdf(h, p);
+    if (s) return s;
+    h->shard_cdf_ep = h->ep_res;
+  }
+  HIPCHK(h->ops->shard_offspring(h->x[h->cx], h->N, h->Npad, h->cdf, U, lo, mass, h->n_total, a, n, out, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+pf_status pf_shard_adopt(pf_handle* h, const void* rows, double* mean, double* cov) {
+  if (!h || !rows) return fail(PF_E_ARG, "null argument");
+  if (!h->sharded) return fail(PF_E_ARG, "pf_shard_adopt needs pf_shard_configure");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, h->seed,
+                             (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream));
+  h->pending = false;
+  h->shard_cdf_ep = 0;
+  if (mean || cov) return pf_moments(h, mean, cov);
+  HIPCHK(hipStreamSynchronize(h->stream));
   return PF_OK;
 }
 

@@ -220,6 +220,11 @@ struct StepParams {
   int rep_base;           // global id of replicate 0 of this launch (Philox counter word)
   int lq_local, lj_local; // chol(Q) / jitter factor block-diagonal in the lane blocks of k_step_grp
   int sys_cdf;            // systematic ancestors searched in the materialised CDF `cdf` (k_step_grp)
+  // within-filter sharding (pf_shard.h): global index of local particle 0 (Philox counters) and
+  // the global log normaliser of the previous weights (replaces the local one when use_lse_ext)
+  int64_t pbase;
+  double lse_ext;
+  int use_lse_ext;
 };
 
 struct Head {
@@ -439,13 +444,14 @@ __device__ __forceinline__ int prefix_tile(const double* Pl, int G, double pos) 
 // NX normals of particle i (flat indices i*NX .. i*NX+NX-1) from Philox, or replay
 template <int NX, typename Real>
 __device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t lrep, uint32_t rep, uint32_t ep,
-                                             uint32_t stream, const double* replay, int64_t N, Real* n) {
+                                             uint32_t stream, const double* replay, int64_t N, Real* n,
+                                             int64_t pbase = 0) {
   if (replay) {
 #pragma unroll
     for (int d = 0; d < NX; ++d) n[d] = (Real)replay[((int64_t)lrep * N + i) * NX + d];
     return;
   }
-  const int64_t f0 = i * NX, f1 = f0 + NX - 1;
+  const int64_t f0 = (i + pbase) * NX, f1 = f0 + NX - 1;  // pbase: global index of local particle 0 (shards)
   constexpr int GMAX = (NX % 4 == 0) ? NX / 4 : NX / 4 + 2;
 #pragma unroll
   for (int gg = 0; gg < GMAX; ++gg) {
@@ -462,13 +468,14 @@ __device__ __forceinline__ void fill_normals(uint64_t seed, int64_t i, uint32_t 
 // normals of scalar particles i0..i0+3 (flat indices i0..i0+3 = one Philox group)
 template <typename Real>
 __device__ __forceinline__ void chunk_normals4(uint64_t seed, int64_t i0, uint32_t lrep, uint32_t rep, uint32_t ep,
-                                               uint32_t stream, const double* replay, int64_t N, Real* n) {
+                                               uint32_t stream, const double* replay, int64_t N, Real* n,
+                                               int64_t pbase = 0) {
   if (replay) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) n[e] = (i0 + e < N) ? (Real)replay[(int64_t)lrep * N + i0 + e] : Real(0);
     return;
   }
-  const Normal4<Real> q = normal4<Real>(seed, (uint32_t)(i0 >> 2), rep, ep, stream);
+  const Normal4<Real> q = normal4<Real>(seed, (uint32_t)((i0 + pbase) >> 2), rep, ep, stream);  // pbase % 4 == 0
 #pragma unroll
   for (int e = 0; e < 4; ++e) n[e] = q.v[e];
 }
@@ -655,7 +662,8 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
         if (p.do_update) load4<Real>(lw_in + i0, sl);
         if (p.do_predict) {
           Real n4[4];
-          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4);
+          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4,
+                               p.pbase);
 #pragma unroll
           for (int e = 0; e < 4; ++e) sn[e][0] = n4[e];
         }
@@ -663,7 +671,9 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
 #pragma unroll
         for (int d = 0; d < NX; ++d) sx[0][d] = x_in[(int64_t)d * p.Npad + i0];
         if (p.do_update) sl[0] = lw_in[i0];
-        if (p.do_predict) fill_normals<NX, Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, sn[0]);
+        if (p.do_predict)
+          fill_normals<NX, Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, sn[0],
+                                 p.pbase);
       }
 #pragma unroll
       for (int e = 0; e < SC; ++e) {
@@ -753,7 +763,7 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
   double aux[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) aux[i] = 0.0;
-  const double lse_prev = h.uniform ? 0.0 : h.lse;
+  const double lse_prev = h.uniform ? 0.0 : (p.use_lse_ext ? p.lse_ext : h.lse);  // shards: the global lse
   const Real lse_r = (Real)lse_prev;
   const bool write_x = p.do_predict || p.allow_gather;  // gather launches always produce x_out
 
@@ -802,13 +812,15 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
 
     Real nj4[CH], np4[CH];
     if constexpr (CH == 4) {  // one Philox call covers the chunk's 4 scalar particles
-      if (gather && p.regularize) chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4);
+      if (gather && p.regularize)
+        chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4, p.pbase);
       if (p.do_predict) {
         if (first) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) np4[e] = sn[e][0];
         } else {
-          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4);
+          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4,
+                               p.pbase);
         }
       }
     }
@@ -821,7 +833,8 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
         if (p.regularize) {
           Real n[NX];
           if constexpr (CH == 4) n[0] = nj4[e];
-          else fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n);
+          else fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n,
+                                      p.pbase);
           M::add_lower(xe, n, P, M::L::LJ);
         }
         aux[0] += 1.0;
@@ -844,7 +857,8 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
 #pragma unroll
             for (int d = 0; d < NX; ++d) n[d] = sn[0][d];
           } else {
-            fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n);
+            fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n,
+                                   p.pbase);
           }
           M::transition(xe, P, u);
           M::add_lower(xe, n, P, M::L::LQ);
@@ -957,13 +971,13 @@ template <typename Real, int NX>
 __global__ void __launch_bounds__(BLOCK) k_init(Real* x, double* rec, const Real* mean /*[R][NX]*/,
                                                 const Real* Lc /*[R][NX][NX]*/, const double* replay,
                                                 int64_t N, int64_t Npad, int G, uint64_t seed,
-                                                uint32_t epoch, int rep_base) {
+                                                uint32_t epoch, int rep_base, int64_t pbase) {
   using RC = Rec<NX>;
   const int r = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i < N) {
     Real n[NX];
-    fill_normals<NX, Real>(seed, i, (uint32_t)r, (uint32_t)(r + rep_base), epoch, STREAM_INIT, replay, N, n);
+    fill_normals<NX, Real>(seed, i, (uint32_t)r, (uint32_t)(r + rep_base), epoch, STREAM_INIT, replay, N, n, pbase);
     const Real* L = Lc + (int64_t)r * NX * NX;
 #pragma unroll
     for (int d = 0; d < NX; ++d) {

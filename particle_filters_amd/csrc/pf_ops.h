@@ -11,6 +11,7 @@
 
 #include "pf_kernels.h"
 #include "pf_resident.h"
+#include "pf_shard_kernels.h"
 #include "pf_step_grp.h"
 
 namespace pf {
@@ -23,7 +24,8 @@ struct Ops {
   hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
   hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
   hipError_t (*init)(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
-                     int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, hipStream_t);
+                     int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, int64_t pbase,
+                     hipStream_t);
   hipError_t (*moments)(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,
                         int64_t Npad, int R, double* mean, double* cov, hipStream_t);
   void (*prepare)();  // per-device kernel attributes, called once a device is current
@@ -31,6 +33,11 @@ struct Ops {
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
   // cannot be co-resident (the caller then runs the launch-per-step path).
   hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t);
+  // within-filter sharding (pf_shard_kernels.h)
+  hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
+                                double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t);
+  hipError_t (*shard_adopt)(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
+                            int jitter, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase, hipStream_t);
 };
 
 void register_ops(const Ops& o);
@@ -63,11 +70,11 @@ struct Launch {
   }
   static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                          int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch,
-                         int rep_base, hipStream_t s) {
+                         int rep_base, int64_t pbase, hipStream_t s) {
     const int64_t n = N > G ? N : G;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK), (unsigned)R);
     hipLaunchKernelGGL((k_init<Real, NX>), grid, dim3(BLOCK), 0, s, (Real*)x, rec, (const Real*)mean,
-                       (const Real*)Lc, replay, N, Npad, G, seed, epoch, rep_base);
+                       (const Real*)Lc, replay, N, Npad, G, seed, epoch, rep_base, pbase);
     return hipGetLastError();
   }
   static hipError_t moments(const void* x, const void* lw, const double* rec, int G, const double* lse,
@@ -77,6 +84,20 @@ struct Launch {
     if (cov)
       hipLaunchKernelGGL((k_mom_cov<Real, NX>), dim3(NX * NX, R), dim3(BLOCK), 64 * sizeof(double), s,
                          (const Real*)x, (const Real*)lw, rec, Rec<NX>::SIZE, G, lse, N, Npad, mean, cov);
+    return hipGetLastError();
+  }
+  static hipError_t shard_offspring(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
+                                    double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_shard_offspring<Real, NX>), dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                       (const Real*)x, N, Npad, cdf, U, lo, mass, Ntot, a, n, (Real*)out);
+    return hipGetLastError();
+  }
+  static hipError_t shard_adopt(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
+                                int jitter, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase, hipStream_t s) {
+    const int64_t n = N > G ? N : G;
+    hipLaunchKernelGGL((k_shard_adopt<Real, NX, NZ, TK, OK>), dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                       s, (const Real*)rows, (Real*)x, N, Npad, rec, G, (const Real*)P, jitter, seed, rep, ep, pbase);
     return hipGetLastError();
   }
   static Ops make(int prec) {
@@ -96,6 +117,8 @@ struct Launch {
     o.moments = &moments;
     o.prepare = &prepare;
     o.resident = nullptr;
+    o.shard_offspring = &shard_offspring;
+    o.shard_adopt = &shard_adopt;
     return o;
   }
   static void prepare() {

@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
   double aux0 = 0.0, auxj[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) auxj[j] = 0.0;
-  const double lse_prev = h.uniform ? 0.0 : h.lse;
+  const double lse_prev = h.uniform ? 0.0 : (p.use_lse_ext ? p.lse_ext : h.lse);  // shards: the global lse
   const Real lse_r = (Real)lse_prev;
   const bool write_x = p.do_predict || p.allow_gather;
   for (int c = vt; c < nchunks; c += VB) {
@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
 #pragma unroll
           for (int j = 0; j < PER; ++j) n[j] = (Real)p.rp_jit[((int64_t)r * p.N + i) * NX + q * PER + j];
         } else {
-          grp_normals<Real, PER>(p.seed, i * NX + q * PER, rep, p.ep_resample, STREAM_JITTER, n);
+          grp_normals<Real, PER>(p.seed, (i + p.pbase) * NX + q * PER, rep, p.ep_resample, STREAM_JITTER, n);
         }
         grp_add_lower<Real, NX, QL>(x, n, P, M::L::LJ, q, base);
       }
@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
 #pragma unroll
         for (int j = 0; j < PER; ++j) n[j] = (Real)p.rp_noise[((int64_t)r * p.N + i) * NX + q * PER + j];
       } else {
-        grp_normals<Real, PER>(p.seed, i * NX + q * PER, rep, p.ep_predict, STREAM_PROCESS, n);
+        grp_normals<Real, PER>(p.seed, (i + p.pbase) * NX + q * PER, rep, p.ep_predict, STREAM_PROCESS, n);
       }
       grp_transition<Real, NX, NZ, TK>(x, P, u, q, base);
       grp_add_lower<Real, NX, QL>(x, n, P, M::L::LQ, q, base);

@@ -19,7 +19,7 @@ from particle_filters_amd import _native as NV
 from particle_filters_amd import models as M
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(REPO, "include", h) for h in ("pf_engine.h", "pf_ledh.h", "pf_edh.h", "pf_diag.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("pf_engine.h", "pf_ledh.h", "pf_edh.h", "pf_diag.h", "pf_shard.h")]
 
 
 def header_functions():
