@@ -5,7 +5,9 @@
 // the whole T loop on the device (pf_ledh_run) with no host synchronisation inside T.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -15,6 +17,7 @@
 #include "pf_ledh_kernels.h"
 #include "pf_diag.h"
 #include "pf_edh_kernels.h"
+#include "pf_ledh_fused.h"
 
 namespace pf {
 // the engine's thread-local error message (pf_last_error, pf_engine.hip)
@@ -53,6 +56,10 @@ struct LOps {
   // EDH (pf_edh_kernels.h): composed flow maps of n_steps time steps; the particle kernel (nonlinear h)
   hipError_t (*edh_setup)(const FlowParams&, double*, int, hipStream_t);
   hipError_t (*flow_edh)(const FlowParams&, hipStream_t);
+  // the whole shared-path step in one cooperative launch (pf_ledh_fused.h); null for nonlinear h
+  hipError_t (*fused)(const FusedParams&, hipStream_t);
+  int (*fused_blocks_per_cu)();
+  int fused_E;  // moment partial entries per workgroup
 };
 
 template <int NX, int NZ, int TK, int OK>
@@ -124,6 +131,26 @@ struct LL {
                        Xp);
     return hipGetLastError();
   }
+  static hipError_t fused(const FusedParams& p, hipStream_t s) {
+    if constexpr (OK == PF_OBS_LINEAR) {
+      hipLaunchKernelGGL((k_ledh_fused<NX, NZ, TK>), dim3(p.nbk), dim3(FusedBlk<NX>::FB), 0, s, p);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
+  static int fused_blocks_per_cu() {
+    if constexpr (OK == PF_OBS_LINEAR) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_ledh_fused<NX, NZ, TK>, FusedBlk<NX>::FB,
+                                                       0) !=
+          hipSuccess)
+        return 0;
+      return nb;
+    } else {
+      return 0;
+    }
+  }
   static hipError_t edh_setup(const FlowParams& p, double* table, int n_steps, hipStream_t s) {
     hipLaunchKernelGGL((k_edh_setup<NX, NZ, TK, OK>), dim3(n_steps), dim3(SB), 0, s, p, table);
     return hipGetLastError();
@@ -140,6 +167,9 @@ struct LL {
     LOps o;
     o.ekf = &ekf;
     o.edh_setup = &edh_setup;
+    o.fused = (OK == PF_OBS_LINEAR) ? &fused : nullptr;
+    o.fused_blocks_per_cu = &fused_blocks_per_cu;
+    o.fused_E = Mom<NX>::E;
     o.flow_edh = &flow_edh;
     o.nx = NX; o.nz = NZ; o.tk = TK; o.ok = OK;
     o.psize = Lay<NX, NZ>::SIZE;
@@ -250,6 +280,11 @@ struct pf_ledh_handle {
   double* mean_prev = nullptr;  // shift of the one-pass moments (ping-pong with mean)
   double *cpart = nullptr, *Pm = nullptr, *Pk = nullptr, *z = nullptr, *u = nullptr, *vbuf = nullptr;
   double* xbar = nullptr;  // EDH: tracker past mean of the current step
+  // fused shared-path step (pf_ledh_fused.h): grid geometry, barrier words, partials
+  int fused_nbk = 0, fused_ppb = 0;
+  unsigned long long fphase = 0;
+  unsigned long long *fwords = nullptr, *fpart = nullptr, *fcpart = nullptr;
+  unsigned int* ferr = nullptr;
   double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
 };
 
@@ -488,6 +523,27 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
       hipMemcpy(h->d_lams, h->lams.data(), h->lams.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
     return bail("upload");
   if (algo == 1 && hipMalloc((void**)&h->xbar, (size_t)nx * 8) != hipSuccess) return bail("xbar");
+  // fused step geometry: <= one workgroup per CU, all co-resident (PF_LEDH_FUSED=0 disables)
+  {
+    const char* env = std::getenv("PF_LEDH_FUSED");
+    const bool want = ops->fused && (h->shared || algo == 1) && !(env && env[0] == '0');
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    const int per_cu = want ? ops->fused_blocks_per_cu() : 0;
+    int64_t ppb = 64;
+    while ((h->N + ppb - 1) / ppb > FMAX && ppb < FPPB) ppb += 64;
+    const int64_t nbk = (h->N + ppb - 1) / ppb;
+    if (want && nbk <= FMAX && nbk <= (int64_t)per_cu * cus) {
+      h->fused_nbk = (int)nbk;
+      h->fused_ppb = (int)ppb;
+      if (hipMalloc((void**)&h->fwords, FMAX * 8) != hipSuccess || hipMalloc((void**)&h->fpart, 4 * FMAX * 8) != hipSuccess ||
+          hipMalloc((void**)&h->fcpart, (size_t)FMAX * ops->fused_E * 8) != hipSuccess ||
+          hipMalloc((void**)&h->ferr, 8) != hipSuccess)
+        return bail("fused step buffers");
+      (void)hipMemset(h->fwords, 0, FMAX * 8);
+      (void)hipMemset(h->ferr, 0, 8);
+    }
+  }
   *out = h;
   return PF_OK;
 }
@@ -520,6 +576,8 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
   for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
                     h->xbar})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)h->fwords, (void*)h->fpart, (void*)h->fcpart, (void*)h->ferr})
     if (p) (void)hipFree(p);
   if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->side) (void)hipStreamDestroy(h->side);
@@ -819,6 +877,39 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         st = lfail(PF_E_HIP, "run: stream wait failed");
         break;
       }
+      if (h->fused_nbk > 0 && dTab) {  // the whole step in one launch (pf_ledh_fused.h)
+        FusedParams fp;
+        fp.f = flow_params(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr);
+        fp.f.table = dTab + t * tsz;
+        fp.f.epoch = ++h->epoch;
+        fp.ep_res = ++h->epoch;
+        fp.x_res = h->x;
+        fp.w_out = h->w_alt;
+        fp.shift = h->mean_prev;
+        fp.mean = h->mean;
+        fp.o_mean = dm + t * nx;
+        fp.o_cov = dc + t * nx * nx;
+        fp.o_ess = de + t;
+        fp.o_flag = df + t;
+        fp.stat = h->stat;
+        fp.cdf = h->cdf;
+        fp.words = h->fwords;
+        fp.part = h->fpart;
+        fp.cpart = h->fcpart;
+        fp.err = h->ferr;
+        fp.phase0 = h->fphase;
+        h->fphase += 4;
+        fp.ratio = h->ratio;
+        fp.nbk = h->fused_nbk;
+        fp.ppb = h->fused_ppb;
+        if (h->ops->fused(fp, h->stream) != hipSuccess) {
+          st = lfail(PF_E_HIP, "run: fused step launch failed");
+          break;
+        }
+        std::swap(h->w, h->w_alt);
+        std::swap(h->mean, h->mean_prev);
+        continue;
+      }
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
                         df + t, dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
@@ -829,6 +920,14 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
       st = lfail(PF_E_HIP, "run: stream synchronisation failed");
       break;
+    }
+    if (h->ferr) {
+      unsigned int fe = 0;
+      if (hipMemcpy(&fe, h->ferr, 4, hipMemcpyDeviceToHost) != hipSuccess || fe != 0u) {
+        (void)hipMemset(h->ferr, 0, 8);
+        st = lfail(PF_E_HIP, "run: fused step grid barrier timed out (workgroups not co-resident)");
+        break;
+      }
     }
     std::vector<int32_t> fl((size_t)T);
     if ((means && hipMemcpy(means, dm, (size_t)T * nx * 8, hipMemcpyDeviceToHost) != hipSuccess) ||
@@ -915,3 +1014,10 @@ pf_status pf_ledh_synchronize(pf_ledh_handle* h) {
 int32_t pf_ledh_shared_path(pf_ledh_handle* h) { return (h && h->shared) ? 1 : 0; }
 
 }  // extern "C"
+
+#ifdef PF_STAMPS
+// diagnostic build only: per-workgroup phase stamps of the last fused LEDH step
+extern "C" int pf_debug_stamps_ledh(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pf::ledh::g_ledh_stamps), (size_t)n * sizeof(unsigned long long));
+}
+#endif

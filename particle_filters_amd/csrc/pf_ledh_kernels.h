@@ -652,17 +652,24 @@ __device__ __forceinline__ double group_trans_part(const FlowParams& p, int q, i
   return group_sum<GL>(part);
 }
 
-template <int NX, int NZ, int TK>
-__global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
+// write-through (agent-coherent) fp64 store / load: data handed between workgroups of one launch
+// that may sit on different XCDs (each with its own L2), as in k_resident
+__device__ __forceinline__ void wt_store(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wt_load(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The affine flow of particle i by its lane group (lane q of GL): writes eta_L to x_out
+// (write-through when WT) and returns the unnormalised log weight (valid in every lane of the group).
+template <int NX, int NZ, int TK, bool WT = false>
+__device__ __forceinline__ double flow_affine_particle(const FlowParams& p, int64_t i, int q, int base) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  const int64_t tid = (int64_t)blockIdx.x * TB + threadIdx.x;
-  const int64_t i = tid / GL;
-  if (i >= p.N) return;  // whole groups leave together
-  const int q = (int)(tid % GL);
-  const int lane = threadIdx.x & 63;
-  const int base = lane - q;
   const double* __restrict__ Pm = p.Pm;
   const double* __restrict__ af = p.table + T::aff(p.L);
   double gx[PER], v[PER];
@@ -690,7 +697,8 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
       double acc = af[T::D0 + a];
 #pragma unroll
       for (int k = 0; k < NZ; ++k) acc += af[T::DM + a * NZ + k] * y0[k];
-      p.x_out[(int64_t)a * p.Npad + i] = e0[j] + acc;
+      if constexpr (WT) wt_store(p.x_out + (int64_t)a * p.Npad + i, e0[j] + acc);
+      else p.x_out[(int64_t)a * p.Npad + i] = e0[j] + acc;
       dd[j] = v[j] + acc;
     } else {
       dd[j] = 0.0;
@@ -698,18 +706,28 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
   }
   // ---- log weight (ledh.py:186-190) -----------------------------------------------
   const double part = group_trans_part<NX, NZ>(p, q, base, dd, v);
-  if (q == 0) {
-    double ez[NZ];
+  double ez[NZ];
 #pragma unroll
-    for (int k = 0; k < NZ; ++k) {
-      double yl = af[T::PL + k];
+  for (int k = 0; k < NZ; ++k) {
+    double yl = af[T::PL + k];
 #pragma unroll
-      for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
-      ez[k] = p.z[k] - (yl + Pm[L::C + k]);
-    }
-    const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
-    p.lw[i] = (log(p.w_in[i] + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
+    for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
+    ez[k] = p.z[k] - (yl + Pm[L::C + k]);
   }
+  const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
+  return (log(p.w_in[i] + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
+}
+
+template <int NX, int NZ, int TK>
+__global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
+  constexpr int GL = Grp<NX>::GL;
+  const int64_t tid = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const int64_t i = tid / GL;
+  if (i >= p.N) return;  // whole groups leave together
+  const int q = (int)(tid % GL);
+  const int base = (threadIdx.x & 63) - q;
+  const double l = flow_affine_particle<NX, NZ, TK>(p, i, q, base);
+  if (q == 0) p.lw[i] = l;
 }
 
 // ---------------------------------------------------------------------------

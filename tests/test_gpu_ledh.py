@@ -203,3 +203,42 @@ def test_run_with_device_tracker_equals_host_tracker(name):
     np.testing.assert_array_equal(r1.flags, r2.flags)
     np.testing.assert_allclose(r1.means, r2.means, rtol=0, atol=1e-8 * scale)
     np.testing.assert_allclose(tr1.state.cov, tr2.state.cov, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("algo", ["ledh", "edh"])
+def test_fused_step_equals_kernel_chain(algo, monkeypatch):
+    """run() on the shared path uses the one-launch fused step (pf_ledh_fused.h); with
+    PF_LEDH_FUSED=0 it runs the five-kernel chain.  Same Philox noise and offsets: same
+    resample decisions, posterior means within 1e-9 of the state scale (workgroup-order sums)."""
+    from particle_filters_amd import edh as ED
+
+    om, gm, hm, g = case("l96")
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PF_LEDH_FUSED", flag)
+        ekf = TR.ExtendedKalmanFilter(gm, hm, om.Q, om.R, jac_g=gm.jacobian, jac_h=hm.jacobian)
+        tracker = TR.EKFTracker(ekf, TR.EKFState(np.asarray(g["mean0"], float).copy(),
+                                                 np.asarray(g["cov0"], float).copy(), 0))
+        args = (tracker, gm, hm, hm.jacobian, M.GaussianTransitionDensity(gm, om.Q), M.GaussianLikelihood(hm, om.R),
+                om.R)
+        if algo == "edh":
+            cfg = ED.EDHConfig(n_particles=10000, n_lambda_steps=8, resample_ess_ratio=0.5,
+                               rng=np.random.default_rng(3))
+            pf = ED.EDHFlowPF(*args, cfg, rng_mode="device")
+        else:
+            cfg = LD.LEDHConfig(n_particles=10000, n_lambda_steps=8, resample_ess_ratio=0.5,
+                                rng=np.random.default_rng(3))
+            pf = LD.LEDHFlowPF(*args, cfg, rng_mode="device")
+        st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+        Z = np.concatenate([g["Z"], L96["obs"][5:25]])
+        res = pf.run(st, Z, tracker="device")
+        out[flag] = (res, pf.state.particles, pf.state.weights)
+    (r1, x1, w1), (r0, x0, w0) = out["1"], out["0"]
+    assert r1.flags.sum() >= 2, "the run must exercise the resample path"
+    np.testing.assert_array_equal(r1.flags, r0.flags)
+    np.testing.assert_allclose(r1.ess, r0.ess, rtol=1e-9)
+    scale = max(1.0, float(np.abs(r0.means).max()))
+    np.testing.assert_allclose(r1.means, r0.means, rtol=0, atol=1e-9 * scale)
+    np.testing.assert_allclose(r1.covs, r0.covs, rtol=0, atol=1e-8 * max(1.0, float(np.abs(r0.covs).max())))
+    np.testing.assert_allclose(x1, x0, rtol=0, atol=1e-9 * scale)
+    np.testing.assert_allclose(w1, w0, rtol=1e-9, atol=1e-15)
