@@ -156,7 +156,8 @@ bool choose_geometry(pf_handle* h) {
 // k_step LDS: base | tile CDF (doubles) + ancestor slots (ints) when gathering | epilogue record staging
 size_t step_lds(const pf_handle* h, bool gather) {
   const size_t epi = (size_t)h->ops->rec_size * sizeof(double);
-  const size_t gat = gather ? (size_t)h->tile * (sizeof(double) + sizeof(int)) : 0;
+  size_t gat = gather ? (size_t)h->tile * (sizeof(double) + sizeof(int)) : 0;
+  if (gather && h->sys_cdf) gat += (size_t)SYS_STAGE * h->tile * sizeof(double) + 16;  // staged source tiles
   return base_lds_bytes(h->G) + std::max(epi, gat);
 }
 

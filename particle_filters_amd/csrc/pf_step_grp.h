@@ -19,6 +19,8 @@
 
 namespace pf {
 
+constexpr int SYS_STAGE = 4;  // source tiles of a block's systematic positions staged in LDS (sys_cdf)
+
 template <int NX>
 struct SGrp {
   // lanes per particle: 8 for nx >= 32 (L96: 5 components per lane), else 4 (MAT: one target per lane)
@@ -385,19 +387,42 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
   if (gather) {
     if (p.method == 0 && p.sys_cdf) {
       // the tile of pos from the prefix Pl, then the slot inside that tile's span of the CDF that
-      // k_cdf materialised (tile_cdf arithmetic: the same ancestors as the per-tile path below)
+      // k_cdf materialised (tile_cdf arithmetic: the same ancestors as the per-tile path below).
+      // The source tiles of this block's (monotone) positions are staged in LDS when they are few.
       const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
       const double* C = p.cdf + (int64_t)r * p.N;
-      if (q == 0)
-        for (int c = vt; c < nchunks; c += VB) {
+      __shared__ int krange[2];
+      if (t == 0) {
+        krange[0] = prefix_tile(Pl, p.G, (U + (double)o0) / (double)p.N);
+        krange[1] = prefix_tile(Pl, p.G, (U + (double)(o1 - 1)) / (double)p.N);
+      }
+      __syncthreads();
+      const int klo = krange[0], nk = krange[1] - krange[0] + 1;
+      const bool staged = nk <= SYS_STAGE;
+      double* stg = (double*)(anc_l + ((p.tile + 1) & ~1));  // SYS_STAGE * tile doubles (step_lds)
+      if (staged)
+        for (int e = t; e < nk * p.tile; e += BS) {
+          const int64_t g = (int64_t)klo * p.tile + e;
+          stg[e] = g < p.N ? C[g] : INFINITY;
+        }
+      __syncthreads();
+      for (int c = t; c < nchunks; c += BS) {  // every lane takes a slot (independent searches)
           const double pos = (U + (double)(o0 + c)) / (double)p.N;
           const int k = prefix_tile(Pl, p.G, pos);
           const int64_t s0 = (int64_t)k * p.tile;
           const int len = (int)min((int64_t)p.tile, p.N - s0);
           int lo = 0, hi = len;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pos < C[s0 + mid]) hi = mid; else lo = mid + 1;
+          if (staged && k >= klo && k < klo + nk) {
+            const double* cs = stg + (int64_t)(k - klo) * p.tile;
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (pos < cs[mid]) hi = mid; else lo = mid + 1;
+            }
+          } else {
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (pos < C[s0 + mid]) hi = mid; else lo = mid + 1;
+            }
           }
           anc_l[c] = (int)(s0 + (lo < len ? lo : len - 1));
         }
