@@ -115,6 +115,8 @@ struct pf_handle {
   bool chol_q_ok = true;
   int lq_local = 0, lj_local = 0;  // chol(Q) / 0.001 chol(Q) block-diagonal in nx/4 blocks (k_step_grp)
   int sys_cdf = 0;  // systematic ancestors from the materialised CDF (k_cdf) instead of per-tile scans
+  int h_sel = 0;    // LINEAR h is a component selection (StepParams.hcol2k)
+  int32_t hcol2k[64];
   // within-filter sharding (pf_shard.h): global index of particle 0, filter size, CDF epoch
   bool sharded = false;
   int64_t pbase = 0, n_total = 0;
@@ -189,6 +191,8 @@ StepParams base_params(pf_handle* h) {
   p.lq_local = h->lq_local;
   p.lj_local = h->lj_local;
   p.sys_cdf = h->sys_cdf;
+  p.h_sel = h->h_sel;
+  std::memcpy(p.hcol2k, h->hcol2k, sizeof(p.hcol2k));
   p.pbase = h->pbase;
   p.out_step = -1;
   p.out_post_step = -1;
@@ -503,6 +507,23 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
     };
     h->lq_local = local(lay_LQ);
     h->lj_local = local(lay_LJ);
+  }
+  for (int c = 0; c < 64; ++c) h->hcol2k[c] = -1;
+  if (m->obs_kind == PF_OBS_LINEAR && nx <= 64 && ops->grp) {  // selection H (every row one 1.0)
+    bool sel = true;
+    for (int k = 0; k < nz && sel; ++k) {
+      int ones = 0, col = -1;
+      for (int c = 0; c < nx; ++c) {
+        const double v = P[lay_H + k * nx + c];
+        if (v == 1.0) { ++ones; col = c; }
+        else if (v != 0.0) sel = false;
+      }
+      if (ones != 1 || h->hcol2k[col] != -1) sel = false;
+      else h->hcol2k[col] = k;
+    }
+    h->h_sel = (sel && r_diag) ? 1 : 0;
+    if (!h->h_sel)
+      for (int c = 0; c < 64; ++c) h->hcol2k[c] = -1;
   }
   h->Pd = P;
   if (!choose_geometry(h)) {

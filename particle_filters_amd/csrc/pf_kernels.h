@@ -225,6 +225,11 @@ struct StepParams {
   int64_t pbase;
   double lse_ext;
   int use_lse_ext;
+  // LINEAR h that selects components (every row of H one 1, e.g. L96's x[::4]): the large-state
+  // kernel reads the observed component instead of the H row (h_sel != 0); hcol2k[c] = the
+  // observation of component c or -1
+  int h_sel;
+  int32_t hcol2k[64];
 };
 
 struct Head {

@@ -253,6 +253,29 @@ __device__ __forceinline__ Real grp_loglik(const Real* x, const Real* z, const R
   }
 }
 
+// selection h with diagonal R: each observation is ONE component owned by one lane, so a lane
+// adds the residuals of its own observed components and the group sums the partial quadratic
+// form (3 shuffles instead of the H-row partials + an NZ-wide all-reduce)
+template <typename Real, int NX, int NZ>
+__device__ __forceinline__ Real grp_loglik_sel(const Real* x, const Real* z, const Real* __restrict__ P, int q,
+                                               const int32_t* hcol2k) {
+  using L = ParamLayout<NX, NZ>;
+  constexpr int PER = SGrp<NX>::PER, SGL = SGrp<NX>::GL;
+  Real quad = Real(0);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int k = hcol2k[q * PER + j];
+    if (k >= 0) {
+      const Real zp = x[j] + P[L::C + k];
+      Real y;
+      if constexpr (sizeof(Real) == 4) y = (z[k] - zp) * P[L::ILR + k];
+      else y = (z[k] - zp) / P[L::LR + k * NZ + k];
+      quad += y * y;
+    }
+  }
+  return Real(-0.5) * gsum<SGL>(quad);
+}
+
 // weighted accumulator of one lane: online max, s0, s00 and its PER components' s1
 template <typename Real, int NX>
 struct GAcc {
@@ -523,7 +546,15 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
       grp_add_lower<Real, NX, QL>(x, n, P, M::L::LQ, q, base);
     }
     if (p.do_update) {
-      const Real ll = (p.do_update == 1) ? grp_loglik<Real, NX, NZ, OK, RD>(x, z, P, q, base) : Real(0);
+      Real ll = Real(0);
+      if (p.do_update == 1) {
+        if constexpr (OK == PF_OBS_LINEAR && RD && NX <= 64) {
+          if (p.h_sel) ll = grp_loglik_sel<Real, NX, NZ>(x, z, P, q, p.hcol2k);
+          else ll = grp_loglik<Real, NX, NZ, OK, RD>(x, z, P, q, base);
+        } else {
+          ll = grp_loglik<Real, NX, NZ, OK, RD>(x, z, P, q, base);
+        }
+      }
       lp = lp + ll;
       acc.add(lp, x);
     }
