@@ -12,6 +12,7 @@ from particle_filters_amd import _native as NV, ledh as LD, models as M, simulat
 lib = NV.load()
 lib.pf_debug_stamps_ledh.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 Np = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+noise = sys.argv[2] if len(sys.argv) > 2 else "device"
 sim = S.simulate_lorenz96(nx=40, F=8.0, dt=0.01, spinup_steps=1000, total_steps=60, Np=1, obs_interval=1,
                           obs_fraction=4, obs_error_std=1.0, seed=42)
 g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(sim.H_idx, 40)
@@ -25,7 +26,7 @@ pf = LD.LEDHFlowPF(tr, g, h, h.jacobian, M.GaussianTransitionDensity(g, Q), M.Ga
 st = pf.init_from_gaussian(m0, c0)
 names = {0: "entry", 1: "P1+P2 flow/exp", 2: "B1", 5: "P3 cdf", 6: "B3", 7: "P4 rows+mom", 8: "B4", 9: "P5 final"}
 for T in (10, 30, 50):
-    res = pf.run(pf.state, sim.observations[1:T + 1], tracker="device")
+    res = pf.run(pf.state, sim.observations[1:T + 1], tracker="device", process_noise=noise)
     nb = 256
     buf = (C.c_ulonglong * (nb * 12))()
     assert lib.pf_debug_stamps_ledh(buf, nb * 12) == 0
@@ -33,7 +34,7 @@ for T in (10, 30, 50):
     live = a[:, 0] > 0
     a = a[live]
     rel = (a - a[:, 0].min()) / 100.0
-    print(f"N={Np} T={T} workgroups={live.sum()} last flag={res.flags[-1]}")
+    print(f"noise={noise} N={Np} T={T} workgroups={live.sum()} last flag={res.flags[-1]}")
     for k, nm in names.items():
         col = rel[:, k]
         col = col[col > -1e6]
