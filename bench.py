@@ -115,6 +115,23 @@ class SV(Workload):
                 "synthetic (simulate_sv_1d alpha=0.95 sigma=0.2 beta=1 seed=42, log-squared wiring)")
 
 
+class SV64(SV):
+    """SURVEY 8(d) roofline run for C2: 64 independent SV filters of N=1e6 each per GPU (Philox
+    replicate ids stand for the per-replicate seeds 42+r); the 1 GB working set exceeds the
+    256 MB MALL, so the launch-per-step kernel streams the state through HBM."""
+
+    name, replicates = "sv64", 64
+    defaults = (100, 10)
+    cpu_steps = 6
+
+    def describe(self, world):
+        return (f"SIR bootstrap PF, 1-D SV (BASELINE config 2 roofline run, SURVEY 8d): {self.replicates} "
+                f"independent filters x N=1e6 particles per GPU ({self.replicates * world} total), systematic "
+                "resampling at Neff<0.5N, T=steps",
+                "synthetic (simulate_sv_1d alpha=0.95 sigma=0.2 beta=1 seed=42, log-squared wiring; "
+                "one observation sequence, Philox replicate ids per filter)")
+
+
 class L96(Workload):
     name, n_particles, replicates, nx, nz = "l96", 100_000, 1, 40, 10
     kernel_tmpl = "float,40,10,L96,LINEAR"
@@ -173,7 +190,7 @@ class MAT(Workload):
                 "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
 
 
-WORKLOADS = {"sv": SV, "l96": L96, "mat": MAT, "ledh": None, "edh": None}
+WORKLOADS = {"sv": SV, "sv64": SV64, "l96": L96, "mat": MAT, "ledh": None, "edh": None}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector 157.3 TF of MI355X_MICROARCH.md)
 
 
@@ -466,7 +483,7 @@ def main():
                 log("cpu baseline failed:", repr(e))
         value = Np * Rl * K * world / elapsed
         line = {
-            "metric": METRIC if wl.name == "sv" else f"particle-steps/sec (N×T/s), {wl.name} workload",
+            "metric": METRIC if wl.name in ("sv", "sv64") else f"particle-steps/sec (N×T/s), {wl.name} workload",
             "value": value,
             "unit": "particle-steps/s",
             "n_gpus": world,

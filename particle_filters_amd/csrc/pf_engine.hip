@@ -122,6 +122,9 @@ struct pf_handle {
   int64_t pbase = 0, n_total = 0;
   uint32_t shard_cdf_ep = 0;
   bool needs_cdf() const { return method == 1 || sys_cdf || sharded; }
+  // per-step replicate heads (k_head, StepParams::head): -1 auto, 0 off, 1 on (PF_HEAD)
+  int head_mode = -1;
+  double* head = nullptr;  // [R][HEAD_STRIDE]
   std::vector<double> Pd;     // params (double)
   // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
   unsigned long long* rsync = nullptr;
@@ -227,7 +230,30 @@ void set_outputs(StepParams& p, const OutSlots& s, bool cov_ok) {
   p.o_flag = s.flag;
 }
 
+// Many replicates: every k_step / k_cdf workgroup re-reducing all G records of its
+// replicate costs O(R G^2) record reads per step; past ~2048 workgroups one k_head
+// launch per step reduces them once per replicate (bitwise the same summary).
+bool use_head(const pf_handle* h) {
+  if (h->sharded || h->G > MAXG) return false;
+  if (h->head_mode >= 0) return h->head_mode != 0;
+  return h->R >= 2 && (int64_t)h->R * h->G >= 2048;
+}
+
+// k_head over the records in p.rec_in; its H workgroups also write p's outputs.
+pf_status launch_head(pf_handle* h, const StepParams& p) {
+  const int H = h->nx <= 4 ? 1 : std::max(1, std::min(h->G, 2 * h->nx));  // output fields per workgroup
+  HIPCHK(h->ops->head(p, h->head, dim3((unsigned)H, (unsigned)h->R), base_lds_bytes(h->G), h->stream));
+  return PF_OK;
+}
+
 pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw, bool writes_rec) {
+  p.head = nullptr;
+  if (use_head(h)) {
+    p.rec_in = h->rec[h->crec];
+    pf_status st = launch_head(h, p);
+    if (st) return st;
+    p.head = h->head;
+  }
   p.x_in = h->x[h->cx];
   p.x_out = h->x[h->cx ^ 1];
   p.lw_in = h->lw[h->clw];
@@ -245,6 +271,16 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
 pf_status launch_cdf(pf_handle* h, StepParams p) {
   p.rec_in = h->rec[h->crec];
   p.lw_in = h->lw[h->clw];
+  p.head = nullptr;
+  if (use_head(h)) {  // k_cdf's own view: resampling allowed, no outputs
+    StepParams q = p;
+    q.allow_gather = 1;
+    q.out_step = -1;
+    q.out_post_step = -1;
+    pf_status st = launch_head(h, q);
+    if (st) return st;
+    p.head = h->head;
+  }
   dim3 grid((unsigned)h->G, (unsigned)h->R);
   HIPCHK(h->ops->cdf(p, h->cdf, grid, base_lds_bytes(h->G) + (size_t)h->tile * sizeof(double), h->stream));
   return PF_OK;
@@ -549,6 +585,9 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   }
   if (h->needs_cdf() && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of cdf failed"));
+  if (const char* he = std::getenv("PF_HEAD")) h->head_mode = std::atoi(he) != 0 ? 1 : 0;
+  if (hipMalloc((void**)&h->head, (size_t)h->R * HEAD_STRIDE * sizeof(double)) != hipSuccess)
+    return cleanup(fail(PF_E_HIP, "hipMalloc of replicate heads failed"));
   if (hipMalloc(&h->P, P.size() * h->esz) != hipSuccess || hipMalloc(&h->d_z, (size_t)h->R * nz * h->esz) != hipSuccess ||
       hipMalloc(&h->d_u, (size_t)h->R * nx * h->esz) != hipSuccess ||
       hipMalloc((void**)&h->d_out, out_doubles(h) * sizeof(double)) != hipSuccess)
@@ -568,6 +607,7 @@ void pf_destroy(pf_handle* h) {
     if (h->rec[k]) (void)hipFree(h->rec[k]);
   }
   if (h->rsync) (void)hipFree(h->rsync);
+  if (h->head) (void)hipFree(h->head);
   for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif})
     if (p) (void)hipFree(p);

@@ -230,6 +230,10 @@ struct StepParams {
   // observation of component c or -1
   int h_sel;
   int32_t hcol2k[64];
+  // many-replicate launches: the summary of rec_in computed once per replicate by k_head
+  // ([R][HEAD_STRIDE] doubles); k_step / k_step_grp / k_cdf then read it instead of every
+  // workgroup re-reducing all G records (O(R G^2) -> O(R G) record reads).  Null: in-kernel prologue.
+  const double* head;
 };
 
 struct Head {
@@ -301,6 +305,31 @@ __device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, do
       run += wk[j];
     }
     if (t == 0) Pl[G] = 1.0;
+    __syncthreads();
+  }
+  return h;
+}
+
+// Head of a replicate as k_head stored it (same fields prologue() returns; the
+// prefix Pl[0..G] staged into LDS when this kernel searches it).  want_prefix must
+// be what the caller's own prologue call would have passed.
+constexpr int HEAD_F = 8;  // M, S, S2, Sscan (with prefix), lse, neff, uniform, resample
+constexpr int HEAD_STRIDE = HEAD_F + MAXG + 8;
+template <int BS>
+__device__ __forceinline__ Head load_head(const double* head, int r, int G, bool want_prefix, double* Pl) {
+  const double* o = head + (int64_t)r * HEAD_STRIDE;
+  Head h;
+  h.M = o[0];
+  h.S = o[1];
+  h.S2 = o[2];
+  h.lse = o[4];
+  h.neff = o[5];
+  h.uniform = o[6] != 0.0;
+  h.resample = o[7] != 0.0;
+  const bool pre = want_prefix && h.resample;
+  h.Sscan = pre ? o[3] : h.S;
+  if (pre) {
+    for (int k = threadIdx.x; k <= G; k += BS) Pl[k] = o[HEAD_F + k];
     __syncthreads();
   }
   return h;
@@ -694,10 +723,16 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
   }
 
   // ---- (0) prologue ---------------------------------------------------------
-  const Head h = prologue<NX, BS>(rec_in, p.G, p.N, p.thresh, p.allow_gather != 0, p.force_gather != 0,
-                              p.allow_gather != 0 && p.method == 0, red, Pl);
-  PF_STAMP(1);
-  write_outputs<NX, BS>(p, rec_in, h, r, R, b, p.G, red);
+  Head h;
+  if (p.head) {
+    h = load_head<BS>(p.head, r, p.G, p.allow_gather != 0 && p.method == 0, Pl);
+    PF_STAMP(1);
+  } else {
+    h = prologue<NX, BS>(rec_in, p.G, p.N, p.thresh, p.allow_gather != 0, p.force_gather != 0,
+                         p.allow_gather != 0 && p.method == 0, red, Pl);
+    PF_STAMP(1);
+    write_outputs<NX, BS>(p, rec_in, h, r, R, b, p.G, red);
+  }
   PF_STAMP(2);
   const bool gather = h.resample != 0;
   const double lprev_uniform = -log((double)p.N);
@@ -962,11 +997,44 @@ __global__ void __launch_bounds__(BS) k_cdf(StepParams p, double* cdf_out) {
   double* cdf = smem + lds_tile(p.G);
   const int b = blockIdx.x, r = blockIdx.y;
   const double* rec = p.rec_in + (int64_t)r * Rec<NX>::SIZE * p.G;
-  const Head h = prologue<NX, BS>(rec, p.G, p.N, p.thresh, true, p.force_gather != 0, true, red, Pl);
+  const Head h = p.head ? load_head<BS>(p.head, r, p.G, true, Pl)
+                        : prologue<NX, BS>(rec, p.G, p.N, p.thresh, true, p.force_gather != 0, true, red, Pl);
   if (!h.resample) return;
   const Real* lw = (const Real*)p.lw_in + (int64_t)r * p.Npad;
   const int len = tile_cdf<Real, NX, BS>(lw, rec, p.G, p.N, p.tile, b, h, Pl, cdf, red);
   for (int j = threadIdx.x; j < len; j += BS) cdf_out[(int64_t)r * p.N + (int64_t)b * p.tile + j] = cdf[j];
+}
+
+// ---------------------------------------------------------------------------
+// Head: the summary of rec_in for every replicate (grid H x R), once per step, for
+// the many-replicate launches (StepParams::head).  The same prologue() and block
+// size as the kernels that read it -> bitwise the decision they would compute.
+// Also writes the step's outputs (write_outputs over the H workgroups).
+// ---------------------------------------------------------------------------
+template <int NX, int BS>
+__global__ void __launch_bounds__(BS) k_head(StepParams p, double* head) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* red = smem;
+  double* Pl = smem + LDS_PL;
+  const int b = blockIdx.x, r = blockIdx.y, R = gridDim.y;
+  const double* rec = p.rec_in + (int64_t)r * Rec<NX>::SIZE * p.G;
+  const bool allow = p.allow_gather != 0;
+  const Head h = prologue<NX, BS>(rec, p.G, p.N, p.thresh, allow, p.force_gather != 0, allow, red, Pl);
+  write_outputs<NX, BS>(p, rec, h, r, R, b, gridDim.x, red);
+  if (b != 0) return;
+  double* o = head + (int64_t)r * HEAD_STRIDE;
+  if (threadIdx.x == 0) {
+    o[0] = h.M;
+    o[1] = h.S;
+    o[2] = h.S2;
+    o[3] = h.Sscan;
+    o[4] = h.lse;
+    o[5] = h.neff;
+    o[6] = h.uniform ? 1.0 : 0.0;
+    o[7] = h.resample ? 1.0 : 0.0;
+  }
+  if (allow && h.resample)
+    for (int k = threadIdx.x; k <= p.G; k += BS) o[HEAD_F + k] = Pl[k];
 }
 
 // ---------------------------------------------------------------------------

@@ -23,6 +23,7 @@ struct Ops {
   hipError_t (*step)(const StepParams&, dim3, size_t, hipStream_t);
   hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
   hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
+  hipError_t (*head)(const StepParams&, double* head_out, dim3, size_t, hipStream_t);
   hipError_t (*init)(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                      int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, int64_t pbase,
                      hipStream_t);
@@ -62,6 +63,10 @@ struct Launch {
   }
   static hipError_t finalize(const StepParams& p, int R, hipStream_t s) {
     hipLaunchKernelGGL((k_finalize<NX, BS>), dim3(R), dim3(BS), LDS_RED * sizeof(double), s, p);
+    return hipGetLastError();
+  }
+  static hipError_t head(const StepParams& p, double* out, dim3 grid, size_t smem, hipStream_t s) {
+    hipLaunchKernelGGL((k_head<NX, BS>), grid, dim3(BS), smem, s, p, out);
     return hipGetLastError();
   }
   static hipError_t cdf(const StepParams& p, double* out, dim3 grid, size_t smem, hipStream_t s) {
@@ -113,6 +118,7 @@ struct Launch {
     o.step = &step;
     o.finalize = &finalize;
     o.cdf = &cdf;
+    o.head = &head;
     o.init = &init;
     o.moments = &moments;
     o.prepare = &prepare;

@@ -39,9 +39,12 @@
 
 namespace pf {
 
-constexpr int RBS = 512;           // threads per resident workgroup (8 waves, 2 per SIMD)
+#ifndef PF_RBS
+#define PF_RBS 512
+#endif
+constexpr int RBS = PF_RBS;        // threads per resident workgroup (8 waves, 2 per SIMD)
 constexpr int RNW = RBS / 64;      // waves per workgroup
-constexpr int RPPT = 8;            // particles per thread = two Philox groups
+constexpr int RPPT = 4096 / RBS;   // particles per thread (8 = two Philox groups); tile fixed at 4096
 constexpr int RPV = RPPT / 4;      // float4 vectors per thread
 constexpr int RTILE = RBS * RPPT;  // 4096 particles per workgroup
 constexpr int RMAXG = 256;         // workgroups per replicate (<= CUs: all co-resident)

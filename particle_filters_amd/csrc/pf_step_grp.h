@@ -398,10 +398,16 @@ __global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
   const bool stamp_on = p.do_predict && p.do_update;
   (void)stamp_on;
   PF_STAMP(0);
-  const Head h = prologue<NX, BS>(rec_in, p.G, p.N, p.thresh, p.allow_gather != 0, p.force_gather != 0,
-                                  p.allow_gather != 0 && p.method == 0, red, Pl);
-  PF_STAMP(1);
-  write_outputs<NX, BS>(p, rec_in, h, r, R, b, p.G, red);
+  Head h;
+  if (p.head) {
+    h = load_head<BS>(p.head, r, p.G, p.allow_gather != 0 && p.method == 0, Pl);
+    PF_STAMP(1);
+  } else {
+    h = prologue<NX, BS>(rec_in, p.G, p.N, p.thresh, p.allow_gather != 0, p.force_gather != 0,
+                         p.allow_gather != 0 && p.method == 0, red, Pl);
+    PF_STAMP(1);
+    write_outputs<NX, BS>(p, rec_in, h, r, R, b, p.G, red);
+  }
   PF_STAMP(2);
   const bool gather = h.resample != 0;
   const double lprev_uniform = -log((double)p.N);

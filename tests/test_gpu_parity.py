@@ -289,3 +289,60 @@ def test_global_cdf_systematic_is_bitwise_the_tile_scan(workload, golden_l96, go
     assert np.array_equal(ra.flags, rb.flags)
     assert np.array_equal(ra.means, rb.means)
     assert np.array_equal(xa, xb)
+
+
+@pytest.mark.parametrize("workload,method,reg", [("sv", "systematic", False), ("sv", "multinomial", True),
+                                                 ("l96", "systematic", False), ("mat", "systematic", True)])
+def test_replicate_heads_are_bitwise_the_inkernel_prologue(workload, method, reg, golden_sv, golden_l96,
+                                                           golden_mat, monkeypatch):
+    """Many-replicate launches reduce each replicate's tile records once per step in k_head
+    (PF_HEAD=1) instead of in every workgroup's prologue (PF_HEAD=0); the runs, the step API
+    outputs and the final particles must be identical bit for bit."""
+    if workload == "sv":
+        g, h, Q, R = M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]]
+        Z = np.log(golden_sv["Y0"][1:60] ** 2)[:, None]
+        m0, c0, n, reps = [golden_sv["X0"][0]], [[0.5]], 20011, 5
+    elif workload == "l96":
+        g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+        Q, R = 0.01 * np.eye(40), np.eye(10)
+        Z = golden_l96["obs"][1:30]
+        m0, c0, n, reps = golden_l96["ensemble"][0, 0], 2.0 * np.eye(40), 9011, 3
+    else:
+        g, h = M.CVTransition(4, 1.0), M.AcousticObservation(golden_mat["S"], 10.0, 0.1, 4)
+        Q, R = np.kron(np.eye(4), np.diag([1.0, 1.0, 0.01, 0.01])) * 0.1, 0.01 * np.eye(25)
+        Z = golden_mat["Z"][1:25]
+        m0, c0, n, reps = golden_mat["X"][0].reshape(-1), np.eye(16), 8011, 3
+    runs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("PF_HEAD", flag)
+        b = ParticleFilterBatch(g, h, Q, R, Np=n, n_replicates=reps, seed=23, resample_thresh=0.5,
+                                resample_method=method, regularize_after_resample=reg)
+        b.initialize(m0, c0)
+        r = b.run(Z)
+        runs.append((r, b.particles(), b.weights()))
+    (ra, xa, wa), (rb, xb, wb) = runs
+    assert ra.flags.sum() >= 2
+    for f in ("means", "covs", "neff", "flags", "log_norm", "ess"):
+        va, vb = getattr(ra, f), getattr(rb, f)
+        assert (va is None and vb is None) or np.array_equal(va, vb), f
+    assert np.array_equal(xa, xb) and np.array_equal(wa, wb)
+
+
+@pytest.mark.parametrize("method", ["systematic", "multinomial"])
+def test_forced_heads_step_api_bitwise(method, golden_sv, monkeypatch):
+    """PF_HEAD=1 forces the k_head path on a single filter: the reference's step-by-step API
+    (predict / update / _resample) must not change by a bit."""
+    monkeypatch.setenv("PF_RESIDENT", "0")
+    Z = np.log(golden_sv["Y0"][1:80] ** 2)[:, None]
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("PF_HEAD", flag)
+        pf = pfa.ParticleFilter(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]],
+                                Np=10007, resample_method=method, regularize_after_resample=True,
+                                rng=np.random.default_rng(5), resample_thresh=0.7)
+        pf.initialize([0.1], [[0.5]])
+        steps = [pf.step(Z[t]) for t in range(len(Z))]
+        out.append((np.array([s.mean for s in steps]), np.array([s.cov for s in steps]),
+                    pf.state.particles.copy(), pf.state.weights.copy(), pf.run(Z[:20]).means))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
