@@ -362,8 +362,14 @@ struct GAcc {
 
 // RD: R diagonal (the likelihood streams over k); QL: chol(Q) and the jitter factor are
 // block-diagonal in the lanes' blocks (noise is lane-local).  Variants picked on the host.
+// The fp32 L96-size variant with diagonal R and lane-local noise fits 128 VGPRs: keep
+// it at 4 waves per SIMD (the others need more registers than that).
 template <typename Real, int NX, int NZ, int TK, int OK, bool RD, bool QL>
-__global__ void __launch_bounds__(256) k_step_grp(StepParams p) {
+constexpr int grp_waves_per_eu = (sizeof(Real) == 4 && RD && QL && NX >= 32) ? 4 : 1;
+
+template <typename Real, int NX, int NZ, int TK, int OK, bool RD, bool QL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu<Real, NX, NZ, TK, OK, RD, QL>)))
+k_step_grp(StepParams p) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
   using GA = GAcc<Real, NX>;
