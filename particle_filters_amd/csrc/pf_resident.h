@@ -56,7 +56,10 @@ constexpr int RF = 7;              // record granules: M, S0, S00, S1, S2, A1, A
 #endif
 constexpr int RLAG = PF_RLAG;      // verification lag (steps)
 constexpr unsigned RSPIN_LIMIT = 1u << 24;
-constexpr int RSTAGE = 8192;       // rollback scatter staging chunk (floats of LDS)
+#ifndef PF_RSTAGE
+#define PF_RSTAGE 8192
+#endif
+constexpr int RSTAGE = PF_RSTAGE;  // rollback scatter staging chunk (floats of LDS)
 
 // Diagnostic phase accounting (PF_STAMPS builds only): workgroup 0, thread 0
 // accumulates s_memrealtime ticks (100 MHz) per phase into g_pf_stamps[0..15].
@@ -274,8 +277,8 @@ __device__ __forceinline__ int64_t count_below(double x, double U, int64_t N) {
 // driven: workgroup b owns input tile b (its snapshot in LDS), builds that tile's
 // fp64 CDF segment, and writes each particle into its offspring slots
 // [C(cdf_{j-1}), C(cdf_j)) of the gathered array — no remote tile reads, work per
-// workgroup proportional to its tile's offspring.  Two grid hand-offs: the exact
-// tile sums (for the global prefix), then the gathered array.  The resampled
+// workgroup proportional to its tile's offspring.  One grid hand-off (the
+// gathered array): the global tile prefix comes from the verified records.  The resampled
 // (and jittered) particles of this workgroup's output slots land in sx_slot.
 // Out of line: it runs on ~5% of steps and its fp64 position arithmetic must not
 // occupy registers in the step loop.  Returns false if a hand-off timed out.
@@ -323,33 +326,19 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   const double off = block_excl_scan<RBS>(part, red, &Town);
   offs[t] = off;
   PF_GMARK(6);
-  // ---- hand-off 1: the exact tile sums ----------------------------------------
-  if (t == 0)
-    __hip_atomic_store((gu64*)(tsum + b), (unsigned long long)__double_as_longlong(Town), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const unsigned long long f1 = 2ull * nres - 1, f2 = 2ull * nres;
-  if (t == 0) st_sc1(sflag + b, f1);
-  for (unsigned spins = 0;; ++spins) {
-    int good = 1;
-    if (t < G) good = ld_sc1(sflag + t) >= f1;
-    if (__syncthreads_and(good)) break;
-    if (spins >= RSPIN_LIMIT) {
-      if (t == 0) {
-        *err_sh = 1;
-        atomicOr(err, 2u);
-      }
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
+  // No hand-off for the tile masses: every workgroup already holds all tiles'
+  // verified records {m_g, s0_g} (thread t: tile t), so the global tile prefix is
+  // computed from those; each tile then maps its own fp64 CDF exactly onto its
+  // prefix interval [Pl[b], Pl[b+1]) (the offspring ranges still partition [0, N)).
+  // The xn write-after-read hazard across rollbacks is ordered by the granule
+  // protocol: a rollback is decided only after every workgroup has published a
+  // step computed from its previous gathered read.
   PF_GMARK(7);
   // ---- global tile prefix in fp64 (fixed order: identical in every workgroup) -
   double fg = 0.0, wg = 0.0;
   if (t < G && s0_g > 0.0f) {
     fg = exp((double)m_g - Mx);
-    wg = __longlong_as_double((long long)ld_sc1((const unsigned long long*)(tsum + t))) * fg;
+    wg = (double)s0_g * fg;
   }
   double Stot;
   const double run = block_excl_scan<RBS>(wg, red, &Stot);
@@ -365,7 +354,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // tile takes the contiguous range [C(Pl[b]), C(Pl[b+1])), staged through LDS
   // in chunks and written with coalesced 16-byte sc1 stores.
   const double U = uniform53(seed, 0, rep, ep_res);
-  const double base = Pl[b], hi = Pl[b + 1], c = Ck[b];
+  const double base = Pl[b], hi = Pl[b + 1], c = (Town > 0.0) ? (hi - base) / Town : 0.0;
   const int64_t tile_last = min(o0 + (int64_t)RTILE, N) - 1;
   int64_t cb[RPPT + 1];  // cb[e] .. cb[e+1]: slots of particle i0 + e (empty past the tile)
   {
@@ -413,6 +402,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // ---- hand-off 2: the gathered array -----------------------------------------
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  const unsigned long long f2 = nres;  // one hand-off per rollback: flags count rollbacks
   if (t == 0) st_sc1(sflag + b, f2);
   for (unsigned spins = 0;; ++spins) {
     int good = 1;
@@ -500,6 +490,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   for (int k = 0; k < ParamLayout<NX, NZ>::SIZE; ++k) P[k] = ((const Real*)p.P)[k];
   const int64_t N = p.N;
   const int G = p.G;
+  const bool outwg = b == G - 1;  // the workgroup that writes the step outputs
   const int64_t o0 = (int64_t)b * RTILE;
   const int64_t i0 = o0 + RPPT * (int64_t)t;
   const int64_t rN = (int64_t)r * p.Npad;
@@ -685,10 +676,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
       const double d0 = wave_sum_ud((double)s0_g * f);
       const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
-      const double d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
-      const double d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
-      const double d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
-      const double d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+      // moments only where the outputs are written; aux sums only after a resample
+      double d2 = 0.0, d3 = 0.0, d4 = 0.0, d5 = 0.0;
+      if (outwg) {
+        d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
+        d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
+        if (prev_res) {
+          d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
+          d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+        }
+      }
       const int wgood = __all(good);
       if (lane == 0) {
         cslot[cur][w][0] = Mw;
@@ -768,10 +765,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
         const double d0 = wave_sum_ud((double)s0_g * f);
         const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
-        const double d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
-        const double d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
-        const double d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
-        const double d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+        // moments only where the outputs are written; aux sums only after a resample
+        double d2 = 0.0, d3 = 0.0, d4 = 0.0, d5 = 0.0;
+        if (outwg) {
+          d2 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[3]) * f : 0.0);
+          d3 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[4]) * f : 0.0);
+          if (prev_res) {
+            d4 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[5]) : 0.0);
+            d5 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[6]) : 0.0);
+          }
+        }
         const int wgood = __all(good);
         if (lane == 0) {
           cslot[cur][w][0] = Mw;
