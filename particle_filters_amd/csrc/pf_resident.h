@@ -530,6 +530,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   double Tprev = 0.0;      // absolute log mass of the last verified step
   bool prev_res = false;   // last verified step resampled: next record carries its aux sums
   bool have_aux = false;   // the live state was just gathered
+  bool rec_aux = false;    // the record being published carries the aux sums
   double aux1 = 0.0, aux2 = 0.0;
   bool last_uniform = false;
   bool alive = true;
@@ -577,8 +578,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (computing) {
       const bool pred = !(fo && tstep == 0);
       const uint32_t ep_pred = p.ep0 + (uint32_t)(2 * tstep) - fo;
-      const float* zt = p.z + ((size_t)tstep * R + r) * NZ;
       Real z[NZ];
+      const float* zt = p.z + ((size_t)tstep * R + r) * NZ;
 #pragma unroll
       for (int k = 0; k < NZ; ++k) z[k] = zt[k];
       const Real* u = p.u ? (const Real*)(p.u + ((size_t)tstep * R + r) * NX) : nullptr;
@@ -657,6 +658,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           sT[slot] = tstep;
         }
       }
+      rec_aux = have_aux;
       have_aux = false;
     }
 
@@ -703,7 +705,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 
     // ---------------- publish this workgroup's record ------------------------
     if (computing) {
-      if (w == 0) {  // combine the wave partials (row 0 of wave 0); lanes 0..6 publish
+#ifndef PF_PUBW
+#define PF_PUBW (RNW - 1)
+#endif
+      // combine the wave partials; lanes 0..6 publish.  The last wave does it: waves
+      // 0..RCW-1 carry the verification summaries, so the work is spread over waves.
+      if (w == PF_PUBW) {
         const int j = lane & (RNW - 1);
         const bool inr = lane < RNW;
         const double* ms = mslot[cur][j];
@@ -715,8 +722,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const float t00 = row_sum_f(inr ? (float)v2 * fj * fj : 0.0f);
         const float t1 = row_sum_f(inr ? (float)v3 * fj : 0.0f);
         const float t2 = row_sum_f(inr ? (float)v4 * fj : 0.0f);
-        const double ta1 = row_sum_d(inr ? v5 : 0.0);
-        const double ta2 = row_sum_d(inr ? v6 : 0.0);
+        const double ta1 = rec_aux ? row_sum_d(inr ? v5 : 0.0) : 0.0;
+        const double ta2 = rec_aux ? row_sum_d(inr ? v6 : 0.0) : 0.0;
         if (lane < RF) {  // 7 granules, one sc1 store each (the data is its own flag)
           const float val = lane == 0 ? Mt : lane == 1 ? t0 : lane == 2 ? t00 : lane == 3 ? t1 : lane == 4 ? t2
                           : lane == 5 ? (float)ta1 : (float)ta2;
