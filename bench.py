@@ -29,7 +29,9 @@ Extra JSON fields:
                 (8 nx + 12) on resample steps) of the timed run / its device
                 duration, timed live with HIP events recorded on the engine's own
                 stream; traffic = HBM bytes per step from the committed rocprofv3
-                PMC passes (profiles/pmc_traffic*.json), or null.
+                PMC passes (profiles/pmc_traffic*.json), or null; valu = the
+                kernel's VALU issue floor per step (profiles/pmc_valu_*.json,
+                SQ_INSTS_VALU) and the fraction of the measured step it covers.
   cpu_baseline  the reference CPU path (faithful per-particle restatement in
                 oracle/, bit-identical to the reference) timed on this host's cores
                 on a bounded sample of the same workload.
@@ -68,6 +70,21 @@ def pmc_traffic(workload, kernel):
     if d.get("kernel_short") != kernel:
         return None, None
     return d.get("bytes_per_step"), d.get("source")
+
+
+def pmc_valu(workload, kernel, us_per_step):
+    """VALU issue floor of `kernel` per filter step from the committed PMC summary
+    (tools/pmc_valu.py: SQ_INSTS_VALU x 2 cycles / occupied SIMDs / 2.4 GHz), if present."""
+    path = os.path.join(REPO, "profiles", f"pmc_valu_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    if d.get("kernel_short") != kernel:
+        return None
+    fl = d["issue_floor_us_per_step"]
+    return {"valu_insts_per_step": d["valu_insts_per_step"], "issue_floor_us_per_step": fl,
+            "frac": fl / us_per_step, "simds": d["simds"], "source": d["source"]}
 
 
 class Workload:
@@ -508,7 +525,8 @@ def main():
                          "algorithmic_bytes_per_step": alg_bytes_run / K,
                          "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),
                          "avg_launch_us": step_s * 1e6 * (K if resident else 1), "us_per_step": step_s * 1e6,
-                         "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src},
+                         "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src,
+                         "valu": pmc_valu(wl.name, kname, step_s * 1e6)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
