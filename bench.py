@@ -373,6 +373,28 @@ def cpu_baseline(wl, Z, mean0, cov0):
                       f"restatement (oracle/pf_oracle.py, bit-identical to the reference), {dt:.1f} s"}
 
 
+def cpu_baseline_numpy(wl, Z, mean0, cov0):
+    """SURVEY.md 8(d) CPU variant (2): the same restatement with vectorised NumPy g/h
+    (one array op per step instead of N Python calls), 1 core, on a bounded sample."""
+    from oracle import pf_oracle
+
+    steps = int(os.environ.get("PF_CPU_NUMPY_STEPS", str(wl.cpu_steps * 5)))
+    ssm = wl.oracle_ssm()
+    pf = pf_oracle.SIROracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, Np=wl.n_particles, rng=np.random.default_rng(42),
+                             vectorized=True)
+    pf.initialize(np.asarray(mean0, float), np.asarray(cov0, float))
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(limits=1):  # BLAS (the nx > 1 noise matmul) on one core too
+        t0 = time.perf_counter()
+        for t in range(steps):
+            pf.step(Z[t])
+        dt = time.perf_counter() - t0
+    return {"value": wl.n_particles * steps / dt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{wl.name} N={wl.n_particles:.0e}, 1 replicate, {steps} steps, vectorised NumPy restatement "
+                      f"(oracle/pf_oracle.py vectorized=True, BLAS limited to 1 thread), {dt:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -496,6 +518,8 @@ def main():
             try:
                 cpu = cpu_baseline(wl, Zall[W:], truth_all[W - 1] if W > 0 else mean0, cov0)
                 cpu["cores_on_host"] = os.cpu_count()
+                cpu["numpy_vectorised"] = cpu_baseline_numpy(wl, Zall[W:], truth_all[W - 1] if W > 0 else mean0,
+                                                             cov0)
             except Exception as e:  # keep the bench line even if the baseline leg breaks
                 log("cpu baseline failed:", repr(e))
         value = Np * Rl * K * world / elapsed
