@@ -136,6 +136,17 @@ struct ResParams {
   int regularize, r_diag, rep_base;
 };
 
+// Granules a verifying workgroup reads: every workgroup needs M, S0, S00 (log mass,
+// Neff, decision, rollback prefix); only the output workgroup needs the moment and
+// aux granules (S1, S2, A1, A2).
+__device__ __forceinline__ bool vg_need(int f, bool outwg) {
+#ifdef PF_VG_ALL
+  return true;
+#else
+  return f < 3 || outwg;
+#endif
+}
+
 __device__ __forceinline__ unsigned long long granule(unsigned tag, float v) {
   return ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
 }
@@ -333,7 +344,6 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // The xn write-after-read hazard across rollbacks is ordered by the granule
   // protocol: a rollback is decided only after every workgroup has published a
   // step computed from its previous gathered read.
-  PF_GMARK(7);
   // ---- global tile prefix in fp64 (fixed order: identical in every workgroup) -
   double fg = 0.0, wg = 0.0;
   if (t < G && s0_g > 0.0f) {
@@ -374,6 +384,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
     }
   }
   const int64_t R0 = count_below(base, U, N), R1 = count_below(hi, U, N);
+  PF_GMARK(7);
   for (int64_t cs = R0; cs < R1; cs += RSTAGE) {
     const int64_t ce = min(cs + (int64_t)RSTAGE, R1);
 #pragma unroll
@@ -562,7 +573,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       // read before this iteration's barrier (written iterations ago)
       if (t < G) {
 #pragma unroll
-        for (int f = 0; f < RF; ++f) pg[f] = ld_sc1(vbase + f * RMAXG);
+        for (int f = 0; f < RF; ++f)
+          if (vg_need(f, outwg)) pg[f] = ld_sc1(vbase + f * RMAXG);
       }
       if (computing && v == s_next) {  // verifying the step computed right now (T=1 / drain)
         Fv = F;
@@ -669,7 +681,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       int good = 1;
       if (in) {
 #pragma unroll
-        for (int f = 0; f < RF; ++f) good &= (unsigned)(pg[f] >> 32) == vtag;
+        for (int f = 0; f < RF; ++f)
+          if (vg_need(f, outwg)) good &= (unsigned)(pg[f] >> 32) == vtag;
       }
       m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
       s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
@@ -761,6 +774,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         if (in) {
 #pragma unroll
           for (int f = 0; f < RF; ++f) {
+            if (!vg_need(f, outwg)) continue;
             pg[f] = ld_sc1(vbase + f * RMAXG);
             good &= (unsigned)(pg[f] >> 32) == vtag;
           }

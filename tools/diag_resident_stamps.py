@@ -25,7 +25,7 @@ outs = [torch.zeros((T, 1), dtype=torch.float64, device=dev) for _ in range(4)]
 fl = torch.zeros((T, 1), dtype=torch.int32, device=dev)
 names = ["loop top (prefetch, decision tail)", "compute", "wave partials + barrier", "publish", "verify combine",
          "rollback (total)"]
-rb_names = {6: "rb: own tile CDF", 7: "rb: tile-sum hand-off", 8: "rb: global prefix", 9: "rb: offspring scatter",
+rb_names = {6: "rb: own tile CDF", 7: "rb: offspring counts", 8: "rb: global prefix", 9: "rb: offspring scatter",
             10: "rb: gathered hand-off", 11: "rb: read+jitter", 12: "slow polls"}
 for rep in range(2):
     lib.pf_debug_stamps_sv_zero(16)
