@@ -166,6 +166,14 @@ bool choose_geometry(pf_handle* h) {
   const char* env = std::getenv("PF_CHUNKS_PER_THREAD");
   int64_t tile = tile_min * (env ? std::max(1, std::atoi(env)) : 1);
   if ((h->N + tile - 1) / tile > MAXG) tile = (h->N + MAXG - 1) / MAXG;
+  // many replicates: a whole number of chunk-loop passes per tile.  A partial last pass
+  // costs a whole pass of latency for a few particles, and the R x G grid runs in several
+  // rounds, so fuller tiles cut rounds (MAT 8 x 1e5: tile 196 = 3 passes + 4 particles ->
+  // 256, 216 -> 199 us/step).  One replicate fits one round either way (L96 N = 1e5 measured
+  // 56.3 us at tile 98 vs 57.8 at 128), so it keeps the smaller tiles.
+  const char* rnd = std::getenv("PF_TILE_ROUND");
+  if (!(rnd && std::atoi(rnd) == 0) && h->R >= 2 && tile > tile_min && tile_min * ((tile + tile_min - 1) / tile_min) <= h->ops->tile_max)
+    tile = tile_min * ((tile + tile_min - 1) / tile_min);
   tile = (tile + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
   if (tile > h->N) tile = (h->N + h->ops->ch - 1) / h->ops->ch * h->ops->ch;
   // many replicates: grow small tiles while the grid exceeds ~4096 workgroups (every workgroup
