@@ -679,6 +679,8 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
   constexpr bool PRE = NX <= 4;
   constexpr int SC = PRE ? CH : 1;
   Real sx[SC][NX], sl[SC], sll[SC], sn[SC][NX];
+  Real px[4], pl[4];  // scalar state: the thread's second chunk, loaded with the first
+  bool pre1 = false;
   Real z[NZ];
   if (p.do_update) {
 #pragma unroll
@@ -694,6 +696,17 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) sx[e][0] = v[e];
         if (p.do_update) load4<Real>(lw_in + i0, sl);
+#ifndef PF_NO_PRE1
+        if (t + BS < nchunks)  // two-pass tiles: the second chunk's loads overlap the first's work
+#else
+        if (false)
+#endif
+        {
+          const int64_t i1 = o0 + (int64_t)(t + BS) * CH;
+          load4<Real>(x_in + i1, px);
+          if (p.do_update) load4<Real>(lw_in + i1, pl);
+          pre1 = true;
+        }
         if (p.do_predict) {
           Real n4[4];
           chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4,
@@ -833,11 +846,19 @@ __global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
           ll[e] = sll[SC == CH ? e : 0];
         }
       } else if constexpr (CH == 4) {
-        Real v[4];
-        load4<Real>(x_in + i0, v);
+        if (pre1 && c == t + BS) {  // prefetched before the prologue
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[e][0] = v[e];
-        if (p.do_update && !h.uniform) load4<Real>(lw_in + i0, lraw);
+          for (int e = 0; e < 4; ++e) {
+            x[e][0] = px[e];
+            lraw[e] = pl[e];
+          }
+        } else {
+          Real v[4];
+          load4<Real>(x_in + i0, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e][0] = v[e];
+          if (p.do_update && !h.uniform) load4<Real>(lw_in + i0, lraw);
+        }
       } else {
 #pragma unroll
         for (int d = 0; d < NX; ++d) x[0][d] = x_in[(int64_t)d * p.Npad + i0];

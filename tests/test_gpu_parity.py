@@ -100,6 +100,21 @@ def test_replay_fp64_matches_reference(name, golden_runs, golden_sv, golden_l96,
     np.testing.assert_allclose(out["final_weights"], ref["final_weights"], rtol=1e-8, atol=1e-15)
 
 
+def test_replay_fp64_two_pass_tiles(monkeypatch, golden_runs, golden_sv, golden_l96, golden_mat):
+    """Tiles of two chunk-loop passes per thread (the many-replicate scalar geometry, whose
+    second chunk is loaded before the prologue) reproduce the reference like the default
+    tiles: Np=3000 -> tiles of 2048 + 952 particles."""
+    name = "sv_logsq_multi_reg"
+    monkeypatch.setenv("PF_CHUNKS_PER_THREAD", "2")
+    ref = pf_cases.golden(golden_runs, name)
+    out, _ = run_engine(name, golden_sv, golden_l96, golden_mat, golden_runs, "fp64")
+    assert np.array_equal(out["flags"], ref["flags"]), f"{name}: resample decisions differ"
+    np.testing.assert_allclose(out["means"], ref["means"], rtol=1e-9, atol=1e-9, err_msg=name)
+    np.testing.assert_allclose(out["covs"], ref["covs"], rtol=1e-8, atol=1e-9, err_msg=name)
+    np.testing.assert_allclose(out["neff"], ref["neff"], rtol=1e-9, err_msg=name)
+    np.testing.assert_allclose(out["final_particles"], ref["final_particles"], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("name", ["sv_logsq", "sv_logsq_reg", "sv_logsq_multi_reg", "sv_harness", "sv_it",
                                   "l96", "mat", "linear_sys"])
 def test_replay_fp32_until_first_resample(name, golden_runs, golden_sv, golden_l96, golden_mat):
