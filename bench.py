@@ -224,14 +224,14 @@ def ledh_flops_per_particle(nx, nz, L):
     return rk4 + noise + y0 + L * per_lam + quad
 
 
-def main_ledh(args, world, rank, local, algo="ledh"):
+def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
     """BASELINE config 5: LEDH particle flow on Lorenz-96 d = 40, N = 1e4, 8 lambda steps
     (algo="edh": the same job with the EDH global flow of EDH_particle_filter.py, RK4 integrator)."""
     import torch
 
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -360,7 +360,7 @@ def cpu_baseline(wl, Z, mean0, cov0):
     on a bounded sample: the bench workload (one replicate) for a few steps, 1 core."""
     from oracle import pf_oracle
 
-    steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", str(wl.cpu_steps)))
+    steps = min(int(os.environ.get("PF_CPU_BASELINE_STEPS", str(wl.cpu_steps))), len(Z))
     ssm = wl.oracle_ssm()
     pf = pf_oracle.SIROracle(ssm.g, ssm.h, ssm.Q, ssm.R, Np=wl.n_particles, rng=np.random.default_rng(42))
     pf.initialize(np.asarray(mean0, float), np.asarray(cov0, float))
@@ -378,7 +378,7 @@ def cpu_baseline_numpy(wl, Z, mean0, cov0):
     (one array op per step instead of N Python calls), 1 core, on a bounded sample."""
     from oracle import pf_oracle
 
-    steps = int(os.environ.get("PF_CPU_NUMPY_STEPS", str(wl.cpu_steps * 5)))
+    steps = min(int(os.environ.get("PF_CPU_NUMPY_STEPS", str(wl.cpu_steps * 5))), len(Z))
     ssm = wl.oracle_ssm()
     pf = pf_oracle.SIROracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, Np=wl.n_particles, rng=np.random.default_rng(42),
                              vectorized=True)
@@ -395,52 +395,135 @@ def cpu_baseline_numpy(wl, Z, mean0, cov0):
                       f"(oracle/pf_oracle.py vectorized=True, BLAS limited to 1 thread), {dt:.1f} s"}
 
 
+def oracle_threads():
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+
+
+def rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, eng_means, eng_flags, precision):
+    """The north-star "RMSE vs CPU ref": the fp64 oracle (the reference algorithm, oracle/) run
+    on the engine's own Philox draws (replicate 0, seed 42, the same epochs: initialize, W
+    warm-up steps, the K timed steps), RMSE vs truth over the timed window for both, and
+    |dRMSE|.  Scalar models: the C restatement (oracle/sir_philox.c, OpenMP); others: the NumPy
+    PhiloxSIROracle on a bounded number of steps."""
+    from oracle import sir_philox as SP
+
+    T = W + K
+    truth = np.asarray(truth_all[W:T], float).reshape(K, -1)
+    bm24 = precision == "fp32"
+    t0 = time.perf_counter()
+    if wl.nx == 1:
+        m = SP.sv_logsq_model(ALPHA, SIGMA, BETA)
+        o = SP.run_scalar(m, np.asarray(Zall[:T], float).reshape(-1), N=wl.n_particles, seed=42, rep=0, ep0=2,
+                          mean0=np.asarray(mean0, float).reshape(-1)[0], var0=float(np.asarray(cov0).reshape(-1)[0]),
+                          bm24=bm24)
+        om, of = o["means"][W:T, None], o["flags"][W:T]
+        impl = f"oracle/sir_philox.c (fp64, {oracle_threads()} OpenMP threads)"
+    else:
+        if T * wl.n_particles * wl.nx > 4e8:
+            return {"skipped": f"T={T} steps x N={wl.n_particles} x nx={wl.nx} exceeds the NumPy oracle budget"}
+        from oracle import pf_oracle
+        ssm = wl.oracle_ssm()
+        o = SP.PhiloxSIROracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, seed=42, rep=0, bm24=bm24, Np=wl.n_particles,
+                               vectorized=True)
+        o.initialize(np.asarray(mean0, float).reshape(-1), np.asarray(cov0, float))
+        r = pf_oracle.run_filter(o, np.asarray(Zall[:T], float))
+        om, of = r["means"][W:T], r["flags"][W:T]
+        impl = "oracle/sir_philox.py PhiloxSIROracle (NumPy, fp64)"
+    dt = time.perf_counter() - t0
+    em = np.asarray(eng_means, float).reshape(K, -1)
+    r_e = float(np.sqrt(np.mean((em - truth) ** 2)))
+    r_o = float(np.sqrt(np.mean((om - truth) ** 2)))
+    return {"rmse_engine": r_e, "rmse_ref": r_o, "abs_diff": abs(r_e - r_o), "tolerance": 1e-4,
+            "max_abs_dmean": float(np.max(np.abs(em - om))),
+            "decision_flips": int(np.sum(np.asarray(eng_flags, bool).reshape(-1) != np.asarray(of, bool))),
+            "window": f"steps [{W}, {T}) after initialize (replicate 0)",
+            "ref": impl + ": the reference SIR algorithm (particle_filter.py) on the engine's Philox draws",
+            "ref_seconds": dt, "ref_particle_steps_per_s": wl.n_particles * T / dt,
+            "ref_threads": oracle_threads() if wl.nx == 1 else 1}
+
+
+def spawn_ranks(n):
+    """``bench.py --gpus N`` without a launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1) before this process
+    touches a GPU, wait for them, and return the worst exit code.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+
+    import torch
+
+    have = torch.cuda.device_count()  # does not initialise the HIP runtime on this image
+    if n > have:
+        log(f"bench: --gpus {n} needs {n} HIP devices, {have} visible; refusing")
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
+    ap.add_argument("--precision", choices=("fp32", "fp64"), default="fp32")
+    ap.add_argument("--spawn", action="store_true", help="launch the rank processes even for --gpus 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref", action="store_true", help="skip the rmse_vs_ref oracle leg")
     args = ap.parse_args()
-    if args.workload in ("ledh", "edh"):
-        return main_ledh(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
-                         int(os.environ.get("LOCAL_RANK", "0")))
-    wl = WORKLOADS[args.workload]()
-    K = args.steps if args.steps is not None else wl.defaults[0]
-    W = args.warmup if args.warmup is not None else wl.defaults[1]
-
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # a launcher (torchrun or spawn_ranks) sets WORLD_SIZE: then the RCCL group exists even at world 1
+    use_dist = "WORLD_SIZE" in os.environ
+    if args.workload in ("ledh", "edh"):
+        return main_ledh(args, world, rank, local, algo=args.workload, use_dist=use_dist)
+    wl = WORKLOADS[args.workload]()
+    K = args.steps if args.steps is not None else wl.defaults[0]
+    W = args.warmup if args.warmup is not None else wl.defaults[1]
 
     import torch
 
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from particle_filters_amd import _native as NV
     from particle_filters_amd.batch import ParticleFilterBatch
+    from particle_filters_amd.distributed import gather_summaries
 
-    g, h, Q, R, Zall, truth_all, mean0, cov0 = wl.build(W + K, rank)
+    # the series also covers the CPU baselines' samples (they start at the timed window)
+    cpu_need = 0 if (rank != 0 or args.no_cpu_baseline) else wl.cpu_steps * 5
+    T_data = W + max(K, cpu_need)
+    g, h, Q, R, Zall, truth_all, mean0, cov0 = wl.build(T_data, rank)
     nx, Rl, Np = wl.nx, wl.replicates, wl.n_particles
     dev = torch.device("cuda", local)
+    rdt = torch.float32 if args.precision == "fp32" else torch.float64
 
-    def dz(a):  # [T][nz] shared by every replicate -> [T][R][nz] fp32 in HBM
+    def dz(a):  # [T][nz] shared by every replicate -> [T][R][nz] in HBM, engine precision
         a = np.broadcast_to(np.asarray(a, float)[:, None, :], (a.shape[0], Rl, wl.nz))
-        return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev).contiguous()
+        return torch.tensor(np.ascontiguousarray(a), dtype=rdt, device=dev).contiguous()
 
     dZw, dZ = dz(Zall[:W]), dz(Zall[W:W + K])
     pf = ParticleFilterBatch(g, h, Q, R, Np=Np, n_replicates=Rl, replicate_base=rank * Rl,
-                             seed=42, precision="fp32", device=local)
+                             seed=42, precision=args.precision, device=local)
     pf.initialize(mean0, cov0)
     lib = NV.load()
+    NV.check(lib.pf_set_timing(pf.handle, 1), "pf_set_timing")
 
     def outs(T):
         f64 = dict(dtype=torch.float64, device=dev)
@@ -454,74 +537,101 @@ def main():
                                NV.C.c_void_p(flags.data_ptr()), NV.C.c_void_p(lnorm.data_ptr()))
         NV.check(st, "pf_run_device")
 
-    ow, ot = outs(W), outs(K)
-    width = nx + 2
-    gathered = [torch.zeros((Rl, K, width), dtype=torch.float64, device=dev) for _ in range(world)]
-
     engine_stream = torch.cuda.ExternalStream(lib.pf_stream(pf.handle), device=dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    done = torch.cuda.Event()
 
     def job(dzz, T, o):
-        """One pass of the timed sequence: T filter steps + RCCL gather of the summaries."""
-        ev0.record(engine_stream)
+        """One pass of the timed sequence: T filter steps (outputs written by the kernels in
+        HBM, no host work) and, with several ranks, the RCCL all-gather of the summaries."""
         run(dzz, T, o)
-        ev1.record(engine_stream)
-        NV.check(lib.pf_synchronize(pf.handle))
-        summary = torch.cat([o[0], o[1][:, :, None], o[2][:, :, None].to(torch.float64)], dim=2)  # [T][R][w]
-        summary = summary.transpose(0, 1)
-        if summary.shape[1] < K:
-            summary = torch.nn.functional.pad(summary, (0, 0, 0, K - summary.shape[1]))
-        if dist:
-            dist.all_gather(gathered, summary.contiguous())
-        else:
-            gathered[0].copy_(summary)
+        if dist is None:
+            return None
+        done.record(engine_stream)
+        torch.cuda.current_stream().wait_event(done)
+        means, neff, flags, lnorm = o
+        summ = torch.cat([means, neff[:, :, None], flags[:, :, None].to(torch.float64), lnorm[:, :, None]], 2)
+        return gather_summaries(summ.transpose(0, 1).contiguous(), Rl * world)
 
-    # warm-up: the exact timed sequence (loads torch / RCCL kernels, clocks up the GPU)
-    job(dZw if W > 0 else dZ[:1], max(W, 1), ow if W > 0 else outs(1))
+    ow, ot = outs(W), outs(K)
+    if W > 0:  # warm-up: the same sequence ahead of the timed window (loads kernels, clocks up the GPU)
+        job(dZw, W, ow)
     torch.cuda.synchronize()
+    NV.check(lib.pf_synchronize(pf.handle), "warm-up")
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    job(dZ, K, ot)
+    gathered = job(dZ, K, ot)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    device_ms = ev0.elapsed_time(ev1)  # device time of the K-step run on the engine stream
+    NV.check(lib.pf_synchronize(pf.handle), "timed run")  # raises on a hand-off timeout / all-dead filter
+    ms = NV.C.c_float()
+    NV.check(lib.pf_last_run_ms(pf.handle, NV.C.byref(ms)), "pf_last_run_ms")
+    device_ms = float(ms.value)  # the K-step run's filter kernels on the engine stream
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, device_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
 
-    # posterior quality of every replicate (gathered summaries)
+    # posterior quality of every replicate (gathered summaries on several ranks)
     truth = np.asarray(truth_all[W:W + K], float).reshape(K, nx)
-    allm = torch.cat(gathered).cpu().numpy()  # [world*R][K][width]
-    rmse = [float(np.sqrt(np.mean((allm[r, :, :nx] - truth) ** 2))) for r in range(allm.shape[0])]
+    if gathered is not None:
+        allm = gathered.cpu().numpy()[:, :, :nx]  # [world*R][K][nx]
+    else:
+        allm = np.transpose(ot[0].cpu().numpy(), (1, 0, 2))
+    rmse = [float(np.sqrt(np.mean((allm[r] - truth) ** 2))) for r in range(allm.shape[0])]
     local_flags = ot[2].cpu().numpy()  # [K][R] this rank's resample decisions
     resample_rate = float(local_flags.mean())
 
     # live roofline of the dominant kernel: device time of the timed run
     resident = bool(lib.pf_last_run_resident(pf.handle))
     step_s = device_ms * 1e-3 / K
-    base_b, res_b = 8.0 * nx + 8.0, 8.0 * nx + 12.0  # SURVEY.md 8(d), bytes per particle
+    esz = 4.0 if args.precision == "fp32" else 8.0
+    base_b, res_b = 2 * esz * nx + 2 * esz, 2 * esz * nx + 12.0  # SURVEY.md 8(d) at the storage width
     alg_bytes_run = Np * (K * Rl * base_b + float(local_flags.sum()) * res_b)
     achieved = alg_bytes_run / (device_ms * 1e-3) / 1e9
     kname = "k_resident" if resident else "k_step"
     traffic, traffic_src = pmc_traffic(wl.name, kname)
     G, tile, lds = pf.geometry()
     workload_desc, data_desc = wl.describe(world)
+    real = "float" if args.precision == "fp32" else "double"
 
     if rank == 0:
         cpu = None
+        errors = []
         if world == 1 and not args.no_cpu_baseline:
+            s0 = truth_all[W - 1] if W > 0 else mean0  # the CPU samples start at the timed window
             try:
-                cpu = cpu_baseline(wl, Zall[W:], truth_all[W - 1] if W > 0 else mean0, cov0)
+                cpu = cpu_baseline(wl, Zall[W:], s0, cov0)
                 cpu["cores_on_host"] = os.cpu_count()
-                cpu["numpy_vectorised"] = cpu_baseline_numpy(wl, Zall[W:], truth_all[W - 1] if W > 0 else mean0,
-                                                             cov0)
-            except Exception as e:  # keep the bench line even if the baseline leg breaks
+            except Exception as e:  # keep the line; the error is recorded in it
+                errors.append(f"faithful port: {e!r}")
                 log("cpu baseline failed:", repr(e))
+            try:
+                npv = cpu_baseline_numpy(wl, Zall[W:], s0, cov0)
+                if cpu is None:
+                    cpu = {"value": None, "unit": "particle-steps/s", "cores": 1, "kind": "port"}
+                cpu["numpy_vectorised"] = npv
+            except Exception as e:
+                errors.append(f"numpy restatement: {e!r}")
+                log("cpu numpy baseline failed:", repr(e))
+            if errors and cpu is not None:
+                cpu["errors"] = errors
+        ref = None
+        if not args.no_ref:
+            try:
+                ref = rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, ot[0][:, 0].cpu().numpy(),
+                                  local_flags[:, 0], args.precision)
+                if cpu is not None and wl.nx == 1 and "ref_particle_steps_per_s" in ref:
+                    cpu["c_openmp"] = {"value": ref["ref_particle_steps_per_s"], "unit": "particle-steps/s",
+                                       "cores": ref["ref_threads"], "kind": "port",
+                                       "sample": f"the rmse_vs_ref run: {Np:.0e} particles x {W + K} steps, C "
+                                                 f"restatement (oracle/sir_philox.c, fp64), {ref['ref_seconds']:.1f} s"}
+            except Exception as e:
+                ref = {"error": repr(e)}
+                log("rmse_vs_ref failed:", repr(e))
         value = Np * Rl * K * world / elapsed
         line = {
             "metric": METRIC if wl.name in ("sv", "sv64") else f"particle-steps/sec (N×T/s), {wl.name} workload",
@@ -534,21 +644,25 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": data_desc,
             "config": {"workload": workload_desc, "n_particles": Np, "replicates_per_gpu": Rl,
-                       "parallelism": f"replicates x{world} (independent filters per GPU, RCCL all-gather of summaries)",
+                       "parallelism": f"replicates x{world} (independent filters per GPU"
+                                      + (", RCCL all-gather of summaries)" if dist else ")"),
                        "geometry": {"tiles": G, "tile": tile, "lds_bytes": lds}},
             "rmse": rmse[0],
             "rmse_all_replicates": rmse,
+            "rmse_vs_ref": ref,
             "resample_rate": resample_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"pf::{kname}<{wl.kernel_tmpl}>",
+                         "kernel": f"pf::{kname}<{real},{wl.kernel_tmpl.split(',', 1)[1]}>",
                          "steps_per_launch": K if resident else 1,
                          "algorithmic_bytes_per_step": alg_bytes_run / K,
                          "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),
                          "avg_launch_us": step_s * 1e6 * (K if resident else 1), "us_per_step": step_s * 1e6,
+                         "timing": "HIP events recorded by pf_run_device on the engine stream around its "
+                                   "filter kernels (pf_set_timing / pf_last_run_ms)",
                          "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src,
                          "valu": pmc_valu(wl.name, kname, step_s * 1e6)},
             "cpu_baseline": cpu,
@@ -557,7 +671,7 @@ def main():
     # orderly teardown: torch's wrapper of the engine stream and its events go
     # before the engine destroys that stream (otherwise exit-time handlers can
     # touch a destroyed stream, seen as a segfault at exit under rocprofv3)
-    del ev0, ev1, engine_stream
+    del done, engine_stream
     torch.cuda.synchronize()
     pf.close()
     if dist:

@@ -29,6 +29,7 @@ typedef int32_t pf_status;
 #define PF_E_NOT_PD 3          /* Cholesky failed -> numpy.linalg.LinAlgError */
 #define PF_E_HIP 4             /* HIP runtime error */
 #define PF_E_UNSUPPORTED 5     /* model shape not compiled into this library */
+#define PF_E_NAN 6             /* every particle weight zero or NaN (all-dead filter) -> FloatingPointError */
 
 /* g: transition kinds (pf.py:237 per-particle g(x,u)) */
 #define PF_TRANS_LINEAR 0 /* x' = A x (+ u)                         params: A[nx*nx]         */
@@ -161,6 +162,11 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
  * grid co-resident), 0 if as the launch-per-step loop.  PF_RESIDENT=0 in the
  * environment forces the launch-per-step loop. */
 int32_t pf_last_run_resident(pf_handle* h);
+/* Live kernel timing for the bench: when on, every pf_run_device records HIP events on
+ * the handle's stream right before its first and after its last filter kernel;
+ * pf_last_run_ms waits for the last run and returns the device time between them. */
+pf_status pf_set_timing(pf_handle* h, int32_t on);
+pf_status pf_last_run_ms(pf_handle* h, float* ms);
 /* Geometry of the step launch: tiles per replicate, tile size, dynamic LDS bytes. */
 pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds_bytes);
 

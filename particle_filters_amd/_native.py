@@ -23,6 +23,7 @@ PF_E_ARG = 2
 PF_E_NOT_PD = 3
 PF_E_HIP = 4
 PF_E_UNSUPPORTED = 5
+PF_E_NAN = 6
 
 PF_TRANS_LINEAR = 0
 PF_TRANS_L96 = 1
@@ -112,6 +113,8 @@ SIGNATURES = {
     "pf_profile_steps": (C.c_int32, [_vp, _vp, C.c_int64, C.POINTER(C.c_float)]),
     "pf_geometry": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "pf_last_run_resident": (C.c_int32, [_vp]),
+    "pf_set_timing": (C.c_int32, [_vp, C.c_int32]),
+    "pf_last_run_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
     # include/pf_ledh.h
     "pf_ledh_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(LedhOpts), C.POINTER(_vp)]),
     "pf_ledh_destroy": (None, [_vp]),
@@ -188,6 +191,8 @@ def check(status: int, what: str = "") -> None:
         raise ValueError(msg)
     if status == PF_E_UNSUPPORTED:
         raise NotImplementedError(msg)
+    if status == PF_E_NAN:
+        raise FloatingPointError(msg)
     raise PFError(msg)
 
 

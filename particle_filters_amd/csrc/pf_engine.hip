@@ -149,9 +149,15 @@ struct pf_handle {
   // register-resident whole-run path (k_resident): hand-off words, zeroed per launch
   unsigned long long* rsync = nullptr;
   size_t rsync_bytes = 0;
+  uint32_t res_tag = 0;           // granule tag base of the next resident launch (ResParams::tag0)
+  unsigned long long res_flag = 0; // hand-off flag base of the next resident launch
   bool res_unchecked = false;  // a resident launch whose timeout word is not yet read
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
   bool last_resident = false;  // the last pf_run_device ran k_resident
+  // live kernel timing (pf_set_timing): events recorded on the handle's stream right
+  // before the first and after the last filter kernel of each pf_run_device
+  bool timing = false;
+  hipEvent_t tev[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -417,18 +423,28 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
   const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
   const size_t bytes = (gran_n + 2 * flag_n + 2) * sizeof(unsigned long long);
+  // Tags and flag values grow from launch to launch (ResParams::tag0 / flag0), so the
+  // sync words are zeroed only when allocated or when the 32-bit tag space would wrap.
+  const uint64_t tag_span = 4 * (uint64_t)T + 16;
+  bool zero = false;
   if (h->rsync_bytes < bytes) {
     if (h->rsync) HIPCHK(hipFree(h->rsync));
     h->rsync = nullptr;
     h->rsync_bytes = 0;
     HIPCHK(hipMalloc((void**)&h->rsync, bytes));
     h->rsync_bytes = bytes;
+    zero = true;
   }
+  if ((uint64_t)h->res_tag + tag_span >= 0xFFFFFFFFull) zero = true;
   if (h->pending) {  // a decision taken before this run is applied first (gather-only launch)
     pf_status st = apply_pending(h, nullptr, nullptr, false);
     if (st) return st;
   }
-  HIPCHK(hipMemsetAsync(h->rsync, 0, bytes, h->stream));
+  if (zero) {
+    HIPCHK(hipMemsetAsync(h->rsync, 0, h->rsync_bytes, h->stream));
+    h->res_tag = 0;
+    h->res_flag = 0;
+  }
   ResParams q;
   std::memset(&q, 0, sizeof(q));
   q.x_in = (const float*)h->x[h->cx];
@@ -441,8 +457,9 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.lg = (float*)h->lw[h->clw ^ 1];
   q.gran = h->rsync;
   q.sflag = h->rsync + gran_n;
-  q.tsum = (double*)(h->rsync + gran_n + flag_n);
   q.err = (unsigned int*)(h->rsync + gran_n + 2 * flag_n);
+  q.tag0 = h->res_tag;
+  q.flag0 = h->res_flag;
   q.P = h->P;
   q.z = (const float*)dZ;
   q.u = (const float*)dU;
@@ -464,12 +481,16 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.regularize = h->regularize;
   q.r_diag = h->r_diag;
   q.rep_base = h->rep_base;
+  if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   const hipError_t e = h->ops->resident(q, G, h->R, h->stream);
+  if (h->timing && e == hipSuccess) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   if (e == hipErrorCooperativeLaunchTooLarge) {
     (void)hipGetLastError();
     return PF_OK;  // not co-resident here: launch-per-step path
   }
   if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
+  h->res_tag += (uint32_t)tag_span;
+  h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;
   h->epoch = q.ep0 + (uint32_t)(2 * T) - k;
   h->ep_res = h->epoch - 1;
@@ -489,8 +510,15 @@ pf_status check_resident(pf_handle* h) {
   const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
   unsigned int err = 0;
   HIPCHK(hipMemcpy(&err, (const void*)(h->rsync + gran_n + 2 * flag_n), sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return fail(PF_E_HIP, "k_resident: inter-workgroup hand-off timed out (code " + std::to_string(err) + ")");
-  return PF_OK;
+  if (!err) return PF_OK;
+  // The launch wrote its particles and records in place: the state is unusable.  Poison
+  // the handle (the next call reports "not initialized") and clear the word for reuse.
+  h->initialized = false;
+  HIPCHK(hipMemset((void*)(h->rsync + gran_n + 2 * flag_n), 0, sizeof(err)));
+  if (err & 8u)
+    return fail(PF_E_NAN, "every particle weight is zero or NaN (all-dead filter); call initialize() again");
+  return fail(PF_E_HIP, "k_resident: inter-workgroup hand-off timed out (code " + std::to_string(err) +
+                            "); call initialize() again");
 }
 
 }  // namespace
@@ -661,6 +689,8 @@ void pf_destroy(pf_handle* h) {
     if (h->rec[k]) (void)hipFree(h->rec[k]);
   }
   if (h->rsync) (void)hipFree(h->rsync);
+  for (hipEvent_t e : h->tev)
+    if (e) (void)hipEventDestroy(e);
   if (h->head) (void)hipFree(h->head);
   for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif})
@@ -775,6 +805,10 @@ pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double*
   const double* bn = bc + (size_t)R * nx * nx;
   const double* bl = bn + R;
   const int32_t* bf = (const int32_t*)(bl + R);
+  for (int r = 0; r < R; ++r)
+    if (!(bn[r] > 0.0))  // S == 0 or NaN: no particle has a finite weight
+      return fail(PF_E_NAN, "every particle weight is zero or NaN (replicate " + std::to_string(r) +
+                                "): the filter is dead");
   bool any = false;
   for (int r = 0; r < R; ++r) {
     if (info) {
@@ -859,6 +893,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   p.do_update = 1;
   bool gather_possible = h->pending;  // a pre-run decision is applied by kernel 0
   uint32_t prev_res = h->ep_res;
+  if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int64_t s = 0; s < T; ++s) {
     const bool predict = !(first_update_only && s == 0);
     p.z = (const char*)dZ + (size_t)s * R * h->nz * h->esz;
@@ -898,7 +933,28 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   p.out_post_step = T - 1;
   st = launch_finalize(h, p);
   if (st) return st;
+  if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   h->pending = false;
+  return PF_OK;
+}
+
+pf_status pf_set_timing(pf_handle* h, int32_t on) {
+  if (!h) return fail(PF_E_ARG, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  if (on && !h->tev[0]) {
+    HIPCHK(hipEventCreate(&h->tev[0]));
+    HIPCHK(hipEventCreate(&h->tev[1]));
+  }
+  h->timing = on != 0;
+  return PF_OK;
+}
+
+pf_status pf_last_run_ms(pf_handle* h, float* ms) {
+  if (!h || !ms) return fail(PF_E_ARG, "null argument");
+  if (!h->tev[0]) return fail(PF_E_ARG, "timing was not enabled (pf_set_timing)");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipEventSynchronize(h->tev[1]));
+  HIPCHK(hipEventElapsedTime(ms, h->tev[0], h->tev[1]));
   return PF_OK;
 }
 
@@ -935,14 +991,20 @@ pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int3
   st = check_resident(h);
   if (st) return bail(st);
   std::vector<int32_t> fl((size_t)T * R);
+  std::vector<double> nf((size_t)T * R);
   if ((means && hipMemcpy(means, dm, (size_t)T * R * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
       (covs && dc && hipMemcpy(covs, dc, (size_t)T * R * nx * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
-      (neff && hipMemcpy(neff, dn, (size_t)T * R * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      hipMemcpy(nf.data(), dn, nf.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
       (lse && hipMemcpy(lse, dl, (size_t)T * R * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
       hipMemcpy(fl.data(), df, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
     return bail(fail(PF_E_HIP, "pf_run: output copy failed"));
   if (flags)
     for (size_t i = 0; i < fl.size(); ++i) flags[i] = (uint8_t)(fl[i] != 0);
+  if (neff) std::memcpy(neff, nf.data(), nf.size() * sizeof(double));
+  for (size_t i = 0; i < nf.size(); ++i)
+    if (!(nf[i] > 0.0))
+      return bail(fail(PF_E_NAN, "every particle weight is zero or NaN at step " + std::to_string(i / R) +
+                                     " (replicate " + std::to_string(i % R) + "): the filter is dead"));
   return bail(PF_OK);
 }
 

@@ -152,24 +152,36 @@ void register_mat_models();
 template <int NX, int NZ, int TK, int OK>
 struct ResidentLaunch {
   // Every workgroup of the grid must be co-resident (they hand data to each other
-  // inside the launch).  The grid is checked against the occupancy API (one
-  // 512-thread workgroup per CU needs <= 256 VGPRs and the kernel's LDS) and
-  // launched plainly; PF_COOP=1 uses hipLaunchCooperativeKernel instead (same
-  // residency, plus the runtime's own size check).
+  // inside the launch), so the kernel is launched cooperatively: the runtime checks
+  // the grid against the device's capacity (hipErrorCooperativeLaunchTooLarge -> the
+  // caller runs the launch-per-step path) and dispatches it so that all workgroups
+  // are resident together.  PF_COOP=0 selects a plain launch after the same check
+  // against the occupancy API (cached per device) — for A/B timing only: a plain
+  // launch cannot guarantee residency when other work shares the GPU.
   static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s) {
     const void* fn = (const void*)k_resident<float, NX, NZ, TK, OK>;
-    const char* coop = std::getenv("PF_COOP");
-    if (coop && std::atoi(coop) != 0) {
+    static const int coop = [] {
+      const char* e = std::getenv("PF_COOP");
+      return (e && std::atoi(e) == 0) ? 0 : 1;
+    }();
+    if (coop) {
       ResParams q = p;
       void* args[] = {&q};
       return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
     }
-    int dev = 0, cus = 0, per_cu = 0;
+    static int cached_dev = -1, cached_cap = 0;
+    int dev = 0;
     hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RBS, 0);
     if (e != hipSuccess) return e;
-    if ((long long)G * R > (long long)cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
+    if (dev != cached_dev) {
+      int cus = 0, per_cu = 0;
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RBS, 0);
+      if (e != hipSuccess) return e;
+      cached_dev = dev;
+      cached_cap = cus * per_cu;
+    }
+    if ((long long)G * R > (long long)cached_cap) return hipErrorCooperativeLaunchTooLarge;
     hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
     return hipGetLastError();
   }

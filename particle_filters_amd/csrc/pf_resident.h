@@ -113,10 +113,9 @@ struct ResParams {
   double* rec_fin;      // [R][RS][Gk] k_step records of the exit state
   float* xg;            // [R][Npad] rollback hand-off buffers
   float* lg;
-  unsigned long long* gran;   // [R][RRING][RF][RMAXG] record granules (zeroed per launch)
-  unsigned long long* sflag;  // [R][RMAXG] hand-off flags (zeroed per launch)
-  double* tsum;               // [R][RMAXG] exact tile weight sums published with a hand-off
-  unsigned int* err;          // spin timeout word (zeroed per launch)
+  unsigned long long* gran;   // [R][RRING][RF][RMAXG] record granules, tag = tag0 + sequence + 1
+  unsigned long long* sflag;  // [R][RMAXG] hand-off flags, value = flag0 + rollback count
+  unsigned int* err;          // spin timeout / all-dead word (zeroed at allocation and after a report)
   const void* P;
   const float* z;  // [T][R][NZ]
   const float* u;  // [T][R][NX] or null
@@ -134,6 +133,12 @@ struct ResParams {
   int first_update_only;
   double thresh;
   int regularize, r_diag, rep_base;
+  // Launch-unique bases of the granule tags and hand-off flag values: the handle
+  // advances them past everything a launch can publish (tags <= 3T + 2 per launch,
+  // flags <= T), so words left by earlier launches never match and the sync words
+  // need no zeroing launch per launch (no memset in front of the kernel).
+  uint32_t tag0;
+  unsigned long long flag0;
 };
 
 // Granules a verifying workgroup reads: every workgroup needs M, S0, S00 (log mass,
@@ -294,7 +299,7 @@ __device__ __forceinline__ int64_t count_below(double x, double U, int64_t N) {
 // Out of line: it runs on ~5% of steps and its fp64 position arithmetic must not
 // occupy registers in the step loop.  Returns false if a hand-off timed out.
 template <typename Real, int NX, int NZ, int TK, int OK>
-__device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, double* tsum, unsigned* err,
+__device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, unsigned long long flag0, unsigned* err,
                                        unsigned* err_sh, float4* sx_slot, const float4* sl_slot, double* red,
                                        double* Pl, double* Ck, double* offs, float* stage, int G, int b, int64_t N,
                                        unsigned nres,
@@ -413,7 +418,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // ---- hand-off 2: the gathered array -----------------------------------------
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const unsigned long long f2 = nres;  // one hand-off per rollback: flags count rollbacks
+  const unsigned long long f2 = flag0 + nres;  // one hand-off per rollback: flags count rollbacks
   if (t == 0) st_sc1(sflag + b, f2);
   for (unsigned spins = 0;; ++spins) {
     int good = 1;
@@ -563,7 +568,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     const int cur = (int)(it & 1u);
     ++it;
     const unsigned v = vnext;
-    const unsigned vtag = v + 1;
+    const unsigned vtag = p.tag0 + v + 1;
     const unsigned long long* vbase = gbase + (size_t)(v % RRING) * RF * RMAXG + t;
     const int idx = (int)(v % NSNAP);  // snapshot slot of step v
     double Fv = 0.0;
@@ -741,7 +746,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           const float val = lane == 0 ? Mt : lane == 1 ? t0 : lane == 2 ? t00 : lane == 3 ? t1 : lane == 4 ? t2
                           : lane == 5 ? (float)ta1 : (float)ta2;
           unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + lane * RMAXG, granule(s_next + 1, val));
+          st_sc1(g + lane * RMAXG, granule(p.tag0 + s_next + 1, val));
         }
       }
       PF_RCOUNT(14);
@@ -839,6 +844,22 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     A1 = uni(A1);
     A2 = uni(A2);
     PF_RMARK(4);
+    if (!(W > 0.0)) {
+      // every particle's weight is zero or NaN (e.g. an all -inf log-likelihood,
+      // SURVEY 8c(vi)): the filter is dead.  Every workgroup reduces the same records
+      // to the same W, so all of them stop here; the host reports PF_E_NAN.
+      if (b == G - 1 && t == 0) {
+        const int64_t o = tv * R + r;
+        p.o_neff[o] = __builtin_nan("");
+        p.o_lse[o] = __builtin_nan("");
+        p.o_mean[o] = __builtin_nan("");
+        if (p.o_cov) p.o_cov[o] = __builtin_nan("");
+        p.o_flag[o] = 0;
+        atomicOr(p.err, 8u);
+      }
+      alive = false;
+      break;
+    }
     const double lse_rel = Mx + log_pos(W);
 #if defined(PF_ABLATE) && PF_ABLATE == 2
     const bool dec = false;  // ablation: never resample (cost of verification without rollbacks)
@@ -876,7 +897,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     PF_RCOUNT(13);
     ++nres;
     const uint32_t ep_res = p.ep0 + (uint32_t)(2 * tv + 1) - fo;
-    if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.sflag + (size_t)r * RMAXG, p.tsum + (size_t)r * RMAXG,
+    if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.sflag + (size_t)r * RMAXG, p.flag0,
                                           p.err, &err_sh, snx[idx], snl[idx], red, Pl, Ck, offs, stage, G, b, N, nres, m_g,
                                           s0_g, Mx, p.seed, rep, ep_res, p.regularize, (const Real*)p.P)) {
       alive = false;
@@ -928,13 +949,13 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         A1 += mslot[0][j][5];
         A2 += mslot[0][j][6];
       }
-      const unsigned tag = s_next + 1;
+      const unsigned tag = p.tag0 + s_next + 1;
       unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
       st_sc1(g + 5 * RMAXG, granule(tag, (float)A1));
       st_sc1(g + 6 * RMAXG, granule(tag, (float)A2));
     }
     // every workgroup's aux granules (fixed-order sum in each workgroup)
-    const unsigned tag = s_next + 1;
+    const unsigned tag = p.tag0 + s_next + 1;
     const unsigned long long* base = gbase + (size_t)(s_next % RRING) * RF * RMAXG + t;
     for (unsigned spins = 0;; ++spins) {
       int good = 1;
