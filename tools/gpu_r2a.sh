@@ -20,7 +20,7 @@ step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench_sv_k20 300 python -u bench.py --steps 20 --warmup 5
 step bench_sv_k20_plain 300 env PF_COOP=0 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref
 step bench_spawn1 300 python -u bench.py --gpus 1 --spawn --steps 20 --warmup 5 --no-cpu-baseline
-step bench_gpus2_refuse 120 python -u bench.py --gpus 2 --steps 20 --warmup 5
+step bench_gpus2_refuse 120 bash -c 'python -u bench.py --gpus 2 --steps 20 --warmup 5; echo exit=$?'
 step bench_sv_fp64 300 python -u bench.py --steps 20 --warmup 5 --precision fp64 --no-cpu-baseline
 step prof_k20 300 rocprofv3 --kernel-trace --stats -d $D/prof_k20 -o sv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref
 step prof_k1000 300 rocprofv3 --kernel-trace --stats -d $D/prof_k1000 -o sv -- python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-ref
