@@ -38,6 +38,9 @@ typedef int32_t pf_status;
 #define PF_OBS_LINEAR 0   /* z = H x + c                            params: H[nz*nx], c[nz]  */
 #define PF_OBS_EXP_HALF 1 /* z_k = beta_k exp(x_k / 2)   (nz==nx)   params: beta[nz]         */
 #define PF_OBS_ACOUSTIC 2 /* z_s = sum_c psi/(|p_c-s|^2+d0) (nx=4C) params: psi, d0, sx[nz], sy[nz] */
+#define PF_OBS_SV_EXACT 3 /* exact SV likelihood y_k ~ N(0, beta_k^2 e^{x_k}) (nz==nx) params: beta[nz];
+                             log p = -x/2 - y^2 e^{-x}/(2 beta^2): test_dpf_vs_sv_simulator.py:60-97.
+                             R is not used (pass any PD matrix, e.g. I). */
 
 #define PF_RESAMPLE_SYSTEMATIC 0 /* pf.py:146-171 */
 #define PF_RESAMPLE_MULTINOMIAL 1 /* pf.py:173-186 (any other method string) */

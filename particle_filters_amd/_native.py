@@ -30,6 +30,7 @@ PF_TRANS_L96 = 1
 PF_OBS_LINEAR = 0
 PF_OBS_EXP_HALF = 1
 PF_OBS_ACOUSTIC = 2
+PF_OBS_SV_EXACT = 3
 PF_RESAMPLE_SYSTEMATIC = 0
 PF_RESAMPLE_MULTINOMIAL = 1
 PF_PRECISION_FP32 = 0

@@ -54,7 +54,7 @@ class ParticleFilterBatch:
         if not M.is_device_model(g, h):
             raise NotImplementedError("ParticleFilterBatch needs particle_filters_amd.models g/h")
         self.Q = np.asarray(Q, float)
-        self.R = np.asarray(R, float)
+        self.R = M.observation_noise(h, R)
         self.nx, self.nz = self.Q.shape[0], self.R.shape[0]
         self.Np = int(Np)
         self.n_replicates = int(n_replicates)

@@ -421,7 +421,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   if (!h->ops->resident || h->method != 0 || h->sharded || !(h->tile == 1024 || h->N <= 1024) || T <= 0) return PF_OK;
   const int G = (int)((h->N + RTILE - 1) / RTILE);
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
-  const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
+  const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
   const size_t bytes = (gran_n + 2 * flag_n + 2) * sizeof(unsigned long long);
   // Tags and flag values grow from launch to launch (ResParams::tag0 / flag0), so the
   // sync words are zeroed only when allocated or when the 32-bit tag space would wrap.
@@ -507,7 +507,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
 pf_status check_resident(pf_handle* h) {
   if (!h->res_unchecked) return PF_OK;
   h->res_unchecked = false;
-  const size_t gran_n = (size_t)h->R * RRING * RF * RMAXG, flag_n = (size_t)h->R * RMAXG;
+  const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
   unsigned int err = 0;
   HIPCHK(hipMemcpy(&err, (const void*)(h->rsync + gran_n + 2 * flag_n), sizeof(err), hipMemcpyDeviceToHost));
   if (!err) return PF_OK;
@@ -568,8 +568,9 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
     if (m->n_obs_params < (int64_t)nz * nx + nz || !m->obs_params) return fail(PF_E_ARG, "LINEAR h needs H[nz*nx], c[nz]");
     for (int i = 0; i < nz * nx; ++i) P[lay_H + i] = m->obs_params[i];
     for (int i = 0; i < nz; ++i) P[lay_C + i] = m->obs_params[nz * nx + i];
-  } else if (m->obs_kind == PF_OBS_EXP_HALF) {
-    if (m->n_obs_params < nz || !m->obs_params) return fail(PF_E_ARG, "EXP_HALF h needs beta[nz]");
+  } else if (m->obs_kind == PF_OBS_EXP_HALF || m->obs_kind == PF_OBS_SV_EXACT) {
+    if (m->n_obs_params < nz || !m->obs_params) return fail(PF_E_ARG, "EXP_HALF / SV_EXACT h needs beta[nz]");
+    if (nz != nx) return fail(PF_E_ARG, "EXP_HALF / SV_EXACT h observes every state component (nz == nx)");
     for (int i = 0; i < nz; ++i) P[lay_C + i] = m->obs_params[i];
   } else if (m->obs_kind == PF_OBS_ACOUSTIC) {
     if (m->n_obs_params < 2 + 2 * nz || !m->obs_params) return fail(PF_E_ARG, "ACOUSTIC h needs psi, d0, sx[nz], sy[nz]");

@@ -1,12 +1,14 @@
 // Scalar stochastic-volatility family: x' = alpha x + sigma n,
 //   h = beta exp(x/2)            (test-harness / standard wiring, PF_OBS_EXP_HALF)
 //   h = log beta^2 + x + E[..]   (log-squared wiring, PF_OBS_LINEAR)
+//   y ~ N(0, beta^2 e^x)         (exact likelihood, PF_OBS_SV_EXACT)
 // plus the 1-D linear test system (h = x) and the 3-D SV of the NLNGSSM notebook.
 #include "pf_ops.h"
 namespace pf {
 void register_sv_models() {
   register_both<1, 1, PF_TRANS_LINEAR, PF_OBS_LINEAR>();
   register_both<1, 1, PF_TRANS_LINEAR, PF_OBS_EXP_HALF>();
+  register_both<1, 1, PF_TRANS_LINEAR, PF_OBS_SV_EXACT>();
   register_both<3, 3, PF_TRANS_LINEAR, PF_OBS_EXP_HALF>();
 }
 }  // namespace pf

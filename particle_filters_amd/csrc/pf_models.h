@@ -7,6 +7,9 @@
 //   observation kinds (h): PF_OBS_LINEAR    z = H x + c            SV log-squared, L96 x[::k], linear tests
 //                          PF_OBS_EXP_HALF  z_k = beta_k exp(x_k/2) SV standard / test-harness wiring
 //                          PF_OBS_ACOUSTIC  z_s = sum_c psi/(|p_c - s|^2 + d0)  (simulator_Multi_acoustic_tracking.py:273-309)
+//                          PF_OBS_SV_EXACT  the exact SV likelihood y_k ~ N(0, beta_k^2 e^{x_k}):
+//                                           log p = -x/2 - y^2 e^{-x} / (2 beta^2) (+ const)
+//                                           (tests/integration_tests/test_dpf_vs_sv_simulator.py:60-97)
 //
 // Parameters live in one read-only array (uniform across the grid -> scalar
 // loads) laid out by ParamLayout<NX, NZ>, in the engine's compute precision.
@@ -81,7 +84,10 @@ struct Model {
 
   // ---- h ------------------------------------------------------------------
   __device__ static __forceinline__ void observe(const Real* x, Real* zp, const Real* __restrict__ P) {
-    if constexpr (OK == PF_OBS_LINEAR) {
+    if constexpr (OK == PF_OBS_SV_EXACT) {  // the observation scale beta e^{x/2} (no Gaussian h)
+#pragma unroll
+      for (int k = 0; k < NZ; ++k) zp[k] = P[L::C + k] * exp(Real(0.5) * x[k]);
+    } else if constexpr (OK == PF_OBS_LINEAR) {
 #pragma unroll
       for (int k = 0; k < NZ; ++k) {
         Real acc = Real(0);
@@ -113,6 +119,25 @@ struct Model {
   // ---- Gaussian log-likelihood: -0.5 |LR^{-1} (z - h(x))|^2 (particle_filter.py:257-261)
   __device__ static __forceinline__ Real loglik(const Real* x, const Real* z, const Real* __restrict__ P,
                                                 bool r_diag) {
+    if constexpr (OK == PF_OBS_SV_EXACT) {
+      // -0.5 sum_k (x_k + y_k^2 e^{-x_k} / beta_k^2): the reference test's log N(y; 0, (beta e^{x/2})^2)
+      // without its constants (pf.py drops the Gaussian constants the same way).  fp32: the product
+      // is one exp of (log(y^2/beta^2) - x), so a far-negative x gives -inf (weight 0) rather than
+      // inf * 0; an all -inf step is caught by the all-dead guard (PF_E_NAN).
+      static_assert(NX == NZ, "SV_EXACT observes every state component");
+      Real quad = Real(0);
+#pragma unroll
+      for (int k = 0; k < NZ; ++k) {
+        const Real b = P[L::C + k];
+        if constexpr (sizeof(Real) == 4) {
+          const Real c = __logf((z[k] * z[k]) / (b * b));  // per step, hoisted out of the particle loop
+          quad += x[k] + __expf(c - x[k]);
+        } else {
+          quad += x[k] + z[k] * z[k] * exp(-x[k]) / (b * b);
+        }
+      }
+      return Real(-0.5) * quad;
+    }
     Real zp[NZ];
     observe(x, zp, P);
     Real y[NZ];

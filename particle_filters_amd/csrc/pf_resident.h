@@ -50,11 +50,26 @@ constexpr int RTILE = RBS * RPPT;  // 4096 particles per workgroup
 constexpr int RMAXG = 256;         // workgroups per replicate (<= CUs: all co-resident)
 constexpr int RCW = RMAXG / 64;    // waves that hold one record each per lane when verifying
 constexpr int RRING = 8;           // record ring slots (>= 2*LAG + 2)
-constexpr int RF = 7;              // record granules: M, S0, S00, S1, S2, A1, A2
+constexpr int RF = 8;              // record granules: M, S0 (high word), S00, S1, S2, A1, A2, S0 (low word)
 #ifndef PF_RLAG
 #define PF_RLAG 2
 #endif
 constexpr int RLAG = PF_RLAG;      // verification lag (steps)
+#ifndef PF_RCOPIES
+#define PF_RCOPIES 8
+#endif
+// Replicas of the record ring.  Every workgroup reads every record of every step: with one
+// copy, ~1000 sc1 loads per step hit the same few lines, i.e. the same memory channels.
+// Writers store all replicas in one instruction (lane = field + RF * replica); reader b uses
+// replica b % RCOPIES.
+constexpr int RCOPIES = PF_RCOPIES;
+static_assert(RF * RCOPIES <= 64, "one publishing wave stores every granule of every replica");
+// elements between replicas: one replica ([R][RRING][RF][RMAXG]) rounded up to 4 KiB, plus
+// 36 KiB, so that the replicas start on different memory channels
+__host__ __device__ inline size_t gran_copy_stride(int R) {
+  const size_t n = (size_t)R * RRING * RF * RMAXG;
+  return (n + 511) / 512 * 512 + 4608;
+}
 constexpr unsigned RSPIN_LIMIT = 1u << 24;
 #ifndef PF_RSTAGE
 #define PF_RSTAGE 8192
@@ -141,19 +156,26 @@ struct ResParams {
   unsigned long long flag0;
 };
 
-// Granules a verifying workgroup reads: every workgroup needs M, S0, S00 (log mass,
-// Neff, decision, rollback prefix); only the output workgroup needs the moment and
-// aux granules (S1, S2, A1, A2).
+// Granules a verifying workgroup reads: every workgroup needs M, S0 (both words), S00
+// (log mass, Neff, decision, rollback prefix); only the output workgroup needs the
+// moment and aux granules (S1, S2, A1, A2).  The tile mass S0 travels as an fp64 value
+// split over two granules: it places the tile's slice of the systematic-resampling CDF
+// (rb_gather), where an fp32 tile mass (~1e-7 relative) would move ~0.1 N slot
+// boundaries per resample against the fp64 reference.
 __device__ __forceinline__ bool vg_need(int f, bool outwg) {
 #ifdef PF_VG_ALL
   return true;
 #else
-  return f < 3 || outwg;
+  return f < 3 || f == 7 || outwg;
 #endif
 }
 
 __device__ __forceinline__ unsigned long long granule(unsigned tag, float v) {
   return ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
+}
+// an fp64 value carried by two granules (payload = high / low 32 bits)
+__device__ __forceinline__ double granule_f64(unsigned long long hi, unsigned long long lo) {
+  return __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
 }
 __device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -303,7 +325,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
                                        unsigned* err_sh, float4* sx_slot, const float4* sl_slot, double* red,
                                        double* Pl, double* Ck, double* offs, float* stage, int G, int b, int64_t N,
                                        unsigned nres,
-                                       float m_g, float s0_g, double Mx, uint64_t seed, uint32_t rep,
+                                       float m_g, double s0_g, double Mx, uint64_t seed, uint32_t rep,
                                        uint32_t ep_res, int regularize, const Real* P) {
   using Mo = Model<Real, NX, NZ, TK, OK>;
   const int t = threadIdx.x;
@@ -351,9 +373,9 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // step computed from its previous gathered read.
   // ---- global tile prefix in fp64 (fixed order: identical in every workgroup) -
   double fg = 0.0, wg = 0.0;
-  if (t < G && s0_g > 0.0f) {
+  if (t < G && s0_g > 0.0) {
     fg = exp((double)m_g - Mx);
-    wg = (double)s0_g * fg;
+    wg = s0_g * fg;
   }
   double Stot;
   const double run = block_excl_scan<RBS>(wg, red, &Stot);
@@ -511,7 +533,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const int64_t i0 = o0 + RPPT * (int64_t)t;
   const int64_t rN = (int64_t)r * p.Npad;
   const float lunif = (float)(-pf_dlog((double)N));
-  const unsigned long long* gbase = p.gran + (size_t)r * RRING * RF * RMAXG;
+  const size_t cstride = gran_copy_stride(R);
+  // this workgroup's replica of its replicate's record ring (reads), and replica 0
+  const unsigned long long* gbase = p.gran + (size_t)(b % RCOPIES) * cstride + (size_t)r * RRING * RF * RMAXG;
+  const unsigned long long* gbase0 = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
 #ifdef PF_STAMPS
   const bool stamp_me = b == 0 && r == 0 && t == 0;
@@ -647,7 +672,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       // wave partials (DPP), one LDS slot per wave
       const float Mw = wave_max_u(m);
       const float fw = (m > -INFINITY) ? __expf(m - Mw) : 0.0f;
-      const float w0 = wave_sum_u(s0 * fw), w00 = wave_sum_u(s00 * fw * fw);
+      const double w0 = wave_sum_ud((double)s0 * (double)fw);  // fp64 tile mass (see vg_need)
+      const float w00 = wave_sum_u(s00 * fw * fw);
       const float w1 = wave_sum_u(s1 * fw), w2 = wave_sum_u(s2 * fw);
       double a1 = 0.0, a2 = 0.0;
       if (have_aux) {
@@ -681,7 +707,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 
     // ---------------- wave-level summary of the step being verified ----------
     const bool in = t < G;
-    float m_g = -INFINITY, s0_g = 0.0f;
+    float m_g = -INFINITY;
+    double s0_g = 0.0;
     if (verify && w < RCW) {
       int good = 1;
       if (in) {
@@ -690,11 +717,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           if (vg_need(f, outwg)) good &= (unsigned)(pg[f] >> 32) == vtag;
       }
       m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
-      s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
-      const float mg = (s0_g > 0.0f) ? m_g : -INFINITY;
+      s0_g = in ? granule_f64(pg[1], pg[7]) : 0.0;
+      const float mg = (s0_g > 0.0) ? m_g : -INFINITY;
       const float Mw = wave_max_u(mg);
       const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
-      const double d0 = wave_sum_ud((double)s0_g * f);
+      const double d0 = wave_sum_ud(s0_g * f);
       const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
       // moments only where the outputs are written; aux sums only after a resample
       double d2 = 0.0, d3 = 0.0, d4 = 0.0, d5 = 0.0;
@@ -736,17 +763,21 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const float mj = inr ? (float)v0 : -INFINITY;
         const float Mt = row_max_f(mj);
         const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
-        const float t0 = row_sum_f(inr ? (float)v1 * fj : 0.0f);
+        const double t0 = row_sum_d(inr ? v1 * (double)fj : 0.0);
         const float t00 = row_sum_f(inr ? (float)v2 * fj * fj : 0.0f);
         const float t1 = row_sum_f(inr ? (float)v3 * fj : 0.0f);
         const float t2 = row_sum_f(inr ? (float)v4 * fj : 0.0f);
         const double ta1 = rec_aux ? row_sum_d(inr ? v5 : 0.0) : 0.0;
         const double ta2 = rec_aux ? row_sum_d(inr ? v6 : 0.0) : 0.0;
-        if (lane < RF) {  // 7 granules, one sc1 store each (the data is its own flag)
-          const float val = lane == 0 ? Mt : lane == 1 ? t0 : lane == 2 ? t00 : lane == 3 ? t1 : lane == 4 ? t2
-                          : lane == 5 ? (float)ta1 : (float)ta2;
-          unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + lane * RMAXG, granule(p.tag0 + s_next + 1, val));
+        if (lane < RF * RCOPIES) {  // RF granules x RCOPIES replicas, one sc1 store (the data is its own flag)
+          const int f = lane % RF, c = lane / RF;
+          const unsigned long long t0b = (unsigned long long)__double_as_longlong(t0);
+          const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(t0b >> 32)
+                             : f == 2 ? __float_as_uint(t00) : f == 3 ? __float_as_uint(t1)
+                             : f == 4 ? __float_as_uint(t2) : f == 5 ? __float_as_uint((float)ta1)
+                             : f == 6 ? __float_as_uint((float)ta2) : (unsigned)t0b;
+          unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+          st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
         }
       }
       PF_RCOUNT(14);
@@ -785,11 +816,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           }
         }
         m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
-        s0_g = in ? __uint_as_float((unsigned)pg[1]) : 0.0f;
-        const float mg = (s0_g > 0.0f) ? m_g : -INFINITY;
+        s0_g = in ? granule_f64(pg[1], pg[7]) : 0.0;
+        const float mg = (s0_g > 0.0) ? m_g : -INFINITY;
         const float Mw = wave_max_u(mg);
         const double f = (mg > -INFINITY) ? (double)__expf(mg - Mw) : 0.0;
-        const double d0 = wave_sum_ud((double)s0_g * f);
+        const double d0 = wave_sum_ud(s0_g * f);
         const double d1 = wave_sum_ud(in ? (double)__uint_as_float((unsigned)pg[2]) * f * f : 0.0);
         // moments only where the outputs are written; aux sums only after a resample
         double d2 = 0.0, d3 = 0.0, d4 = 0.0, d5 = 0.0;
@@ -956,7 +987,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     }
     // every workgroup's aux granules (fixed-order sum in each workgroup)
     const unsigned tag = p.tag0 + s_next + 1;
-    const unsigned long long* base = gbase + (size_t)(s_next % RRING) * RF * RMAXG + t;
+    const unsigned long long* base = gbase0 + (size_t)(s_next % RRING) * RF * RMAXG + t;  // replica 0
     for (unsigned spins = 0;; ++spins) {
       int good = 1;
       unsigned long long g5 = 0, g6 = 0;

@@ -21,6 +21,8 @@ log-squared ``log b^2 + x + E`` (PF_VS notebook cell 6)   ``SVLogSqObservation(b
 ``A @ x (+u)`` / ``H @ x`` (test_pf_shapes_and_api.py)   ``LinearTransition(A)`` / ``LinearObservation(H)``
 ``rk4_step(x, dt, l96_rhs)`` / ``x[H_idx]`` (L96)         ``L96Transition(F, dt, nx)`` / ``SelectObservation(H_idx, nx)``
 MAT joint ``g_joint`` / ``h_joint``                      ``CVTransition(C, dt)`` / ``AcousticObservation(S, psi, d0, C)``
+exact SV ``sv_log_likelihood_fn`` (test_dpf_vs_sv_       ``SVExactObservation(beta)`` (R unused)
+simulator.py:60-97)
 ======================================================  =========================================
 """
 
@@ -245,6 +247,48 @@ class ExpHalfObservation(Observation):
     def jacobian(self, x):
         x = np.atleast_1d(np.asarray(x, float))
         return np.diag(0.5 * self.beta * np.exp(0.5 * x))
+
+
+class SVExactObservation(Observation):
+    """The exact stochastic-volatility likelihood ``y_k ~ N(0, (beta_k e^{x_k/2})^2)``.
+
+    The reference's ``ParticleFilter`` only takes Gaussian ``h``/``R`` wirings; this one is
+    the TensorFlow test's ``sv_log_likelihood_fn``
+    (``tests/integration_tests/test_dpf_vs_sv_simulator.py:60-97``):
+    ``log p(y|x) = -0.5 log 2pi - log(beta e^{x/2}) - 0.5 (y / (beta e^{x/2}))^2``, evaluated
+    on the device without the constants (they cancel in the normalised weights, as pf.py's
+    dropped Gaussian constants do; ``log_norm`` outputs differ from the full log-density by
+    ``-nz (0.5 log 2pi + log beta)`` per step).  Observations are the raw ``Y`` (not log Y^2).
+    ``R`` is not used: pass ``None`` (taken as I) or any positive-definite matrix.
+    Calling the object gives the observation scale ``beta e^{x/2}``."""
+
+    kind = N.PF_OBS_SV_EXACT
+
+    def __init__(self, beta):
+        self.beta = np.atleast_1d(np.asarray(beta, float))
+        self.nx = self.nz = self.beta.size
+
+    def params(self):
+        return np.ascontiguousarray(self.beta)
+
+    def __call__(self, x):
+        x = np.atleast_1d(np.asarray(x, float))
+        return self.beta * np.exp(0.5 * x)
+
+    def log_likelihood(self, y, x):
+        """The full log-density of the reference test (with its constants), per particle."""
+        sig = self(x)
+        y = np.atleast_1d(np.asarray(y, float))
+        return float(np.sum(-0.5 * np.log(2 * np.pi) - np.log(sig) - 0.5 * (y / sig) ** 2))
+
+
+def observation_noise(h, R):
+    """R as the engine takes it: the exact SV likelihood has none (None -> I)."""
+    if R is None:
+        if getattr(h, "kind", None) == N.PF_OBS_SV_EXACT:
+            return np.eye(h.nz)
+        raise ValueError("R is required for a Gaussian observation model")
+    return np.atleast_2d(np.asarray(R, float))
 
 
 class AcousticObservation(Observation):

@@ -136,7 +136,7 @@ class ParticleFilter:
         self.g = g
         self.h = h
         self.Q = np.asarray(Q, float)
-        self.R = np.asarray(R, float)
+        self.R = M.observation_noise(h, R)
         self.Np = int(Np)
         self.resample_thresh = float(resample_thresh)
         self.resample_method = resample_method
