@@ -35,9 +35,10 @@
 extern "C" {
 #endif
 
-/* Make h (R = 1, systematic, N_loc = its n_particles, N_loc % 4 == 0) shard `rank` of a filter of
- * n_total = W * N_loc particles: its particle i is global particle rank * N_loc + i.  Call before
- * pf_initialize. */
+/* Make h (R = 1, systematic, N_loc = its n_particles) shard `rank` of a filter of n_total =
+ * W * N_loc particles: its particle i is global particle rank * N_loc + i.  Call before
+ * pf_initialize.  Device-RNG draws of a scalar-state shard need N_loc % 4 == 0 (its 4-particle
+ * chunks must align with the Philox groups); host-replayed draws take any N_loc. */
 pf_status pf_shard_configure(pf_handle* h, int64_t n_total, int32_t rank);
 
 typedef struct pf_shard_stats {
@@ -59,9 +60,11 @@ pf_status pf_shard_update(pf_handle* h, const double* z, double lse_prev, pf_sha
 pf_status pf_shard_offspring(pf_handle* h, double U, double lo, double mass, int64_t a, int64_t n, void* out);
 
 /* The resampled shard: rows [N_loc][nx] (device, handle precision) become the particles in slot
- * order, weights uniform, + 0.001 chol(Q) jitter when the filter regularises.  mean [nx],
- * cov [nx][nx] (nullable): moments of the adopted particles. */
-pf_status pf_shard_adopt(pf_handle* h, const void* rows, double* mean, double* cov);
+ * order, weights uniform, + 0.001 chol(Q) jitter when the filter regularises: jitter [N_loc][nx]
+ * host normals of this shard's slots (host replay of the reference's draw stream), or NULL for
+ * the device Philox draws of the global slot indices.  mean [nx], cov [nx][nx] (nullable):
+ * moments of the adopted particles. */
+pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, double* mean, double* cov);
 
 #ifdef __cplusplus
 }

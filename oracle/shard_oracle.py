@@ -6,7 +6,8 @@ The CPU stand-in for ``particle_filters_amd.sharded.HipShard`` (the device shard
 Philox normals of GLOBAL particle indices (``oracle/philox.py``), the update of
 ``particle_filter.py:239-263`` with the global normaliser of the previous weights, offspring
 rows of global systematic slots (positions mapped into the shard's CDF segment), adoption
-with uniform weights.  Only ``tests/`` import it.
+with uniform weights and the optional 0.001 chol(Q) jitter; or, in host replay, the
+reference's own normals for its rows.  Only ``tests/`` import it.
 """
 
 from __future__ import annotations
@@ -19,7 +20,7 @@ from oracle import philox
 
 class NumpyShard:
     def __init__(self, ssm, *, nx, n_loc, n_total, rank, thresh, regularize, seed, **_):
-        assert not regularize, "the NumPy shard does not jitter"
+        self.regularize = bool(regularize)
         self.ssm = ssm
         self.nx = nx
         self.n_loc = n_loc
@@ -41,15 +42,16 @@ class NumpyShard:
         n = philox.normals(self.seed, (self.pbase + self.n_loc) * self.nx, 0, epoch, stream)
         return n[self.pbase * self.nx:].reshape(self.n_loc, self.nx)
 
-    def initialize(self, mean, cov):
+    def initialize(self, mean, cov, replay=None):
         L = np.linalg.cholesky(cov + 1e-10 * np.eye(self.nx))
-        self.x = self._normals(philox.STREAM_INIT, self.epoch) @ L.T + mean[None, :]
+        n = self._normals(philox.STREAM_INIT, self.epoch) if replay is None else np.asarray(replay, float)
+        self.x = n @ L.T + mean[None, :]
         self.epoch += 1
         self.l = np.zeros(self.n_loc)
         self.uniform = True
 
-    def predict(self, u):
-        n = self._normals(philox.STREAM_PROCESS, self.epoch)
+    def predict(self, u, replay=None):
+        n = self._normals(philox.STREAM_PROCESS, self.epoch) if replay is None else np.asarray(replay, float)
         self.epoch += 1
         self.x = self.ssm.g_vec(self.x, u) + n @ self.LQ.T
 
@@ -81,8 +83,15 @@ class NumpyShard:
         self.outbox[:n] = torch.from_numpy(self.x[j])
         return self.outbox[:n]
 
-    def adopt(self):
+    def adopt(self, jitter=None):
         self.x = self.inbox.numpy().copy()
+        if self.regularize:  # pf.py:212-218
+            try:
+                Lq = np.linalg.cholesky(self.ssm.Q)
+            except np.linalg.LinAlgError:
+                Lq = np.linalg.cholesky(self.ssm.Q + 1e-12 * np.eye(self.nx))
+            n = self._normals(philox.STREAM_JITTER, self.ep_res) if jitter is None else np.asarray(jitter, float)
+            self.x = self.x + n @ (0.001 * Lq.T)
         self.l = np.zeros(self.n_loc)
         self.uniform = True
         mean = self.x.mean(axis=0)

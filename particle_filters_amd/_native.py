@@ -147,7 +147,7 @@ SIGNATURES = {
     "pf_shard_configure": (C.c_int32, [_vp, C.c_int64, C.c_int32]),
     "pf_shard_update": (C.c_int32, [_vp, _dp, C.c_double, C.POINTER(ShardStats), _dp, _dp]),
     "pf_shard_offspring": (C.c_int32, [_vp, C.c_double, C.c_double, C.c_double, C.c_int64, C.c_int64, _vp]),
-    "pf_shard_adopt": (C.c_int32, [_vp, _vp, _dp, _dp]),
+    "pf_shard_adopt": (C.c_int32, [_vp, _vp, _dp, _dp, _dp]),
 }
 
 _lib = None

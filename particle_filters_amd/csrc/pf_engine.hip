@@ -744,6 +744,8 @@ pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
   if (!h) return fail(PF_E_ARG, "null handle");
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (!h->chol_q_ok) return fail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
+  if (h->sharded && !replay && h->ops->ch > 1 && h->pbase % 4)
+    return fail(PF_E_ARG, "device-RNG predict of a scalar-state shard needs N_loc % 4 == 0 (or host replay)");
   HIPCHK(hipSetDevice(h->device));
   StepParams p = base_params(h);
   if (u) {
@@ -1107,8 +1109,8 @@ pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
 pf_status pf_shard_configure(pf_handle* h, int64_t n_total, int32_t rank) {
   if (!h) return fail(PF_E_ARG, "null handle");
   if (h->R != 1 || h->method != 0) return fail(PF_E_ARG, "sharding needs R = 1 and systematic resampling");
-  if (h->N % 4 != 0 || n_total <= 0 || n_total % h->N != 0 || rank < 0 || (int64_t)rank >= n_total / h->N)
-    return fail(PF_E_ARG, "sharding needs N_loc % 4 == 0, n_total = W * N_loc and 0 <= rank < W");
+  if (n_total <= 0 || n_total % h->N != 0 || rank < 0 || (int64_t)rank >= n_total / h->N)
+    return fail(PF_E_ARG, "sharding needs n_total = W * N_loc and 0 <= rank < W");
   if (n_total / 4 > (int64_t)UINT32_MAX / (h->nx > 0 ? h->nx : 1))
     return fail(PF_E_ARG, "n_total too large for 32-bit Philox counters");
   HIPCHK(hipSetDevice(h->device));
@@ -1181,12 +1183,22 @@ pf_status pf_shard_offspring(pf_handle* h, double U, double lo, double mass, int
   return PF_OK;
 }
 
-pf_status pf_shard_adopt(pf_handle* h, const void* rows, double* mean, double* cov) {
+pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, double* mean, double* cov) {
   if (!h || !rows) return fail(PF_E_ARG, "null argument");
   if (!h->sharded) return fail(PF_E_ARG, "pf_shard_adopt needs pf_shard_configure");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, h->seed,
-                             (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream));
+  const double* rj = nullptr;
+  if (jitter && h->regularize) {  // host replay: this shard's slots' jitter normals [N_loc][nx]
+    pf_status st = ensure_replay(h, &h->d_replay_b, (size_t)h->N * h->nx);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(h->d_replay_b, jitter, (size_t)h->N * h->nx * sizeof(double), hipMemcpyHostToDevice,
+                          h->stream));
+    rj = h->d_replay_b;
+  } else if (h->ops->ch > 1 && h->pbase % 4) {
+    return fail(PF_E_ARG, "device-RNG jitter of a scalar-state shard needs N_loc % 4 == 0 (or host replay)");
+  }
+  HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, rj,
+                             h->seed, (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream));
   h->pending = false;
   h->shard_cdf_ep = 0;
   if (mean || cov) return pf_moments(h, mean, cov);

@@ -38,7 +38,8 @@ struct Ops {
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
                                 double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t);
   hipError_t (*shard_adopt)(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
-                            int jitter, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase, hipStream_t);
+                            int jitter, const double* rp_jit, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase,
+                            hipStream_t);
 };
 
 void register_ops(const Ops& o);
@@ -99,10 +100,12 @@ struct Launch {
     return hipGetLastError();
   }
   static hipError_t shard_adopt(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
-                                int jitter, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase, hipStream_t s) {
+                                int jitter, const double* rp_jit, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase,
+                                hipStream_t s) {
     const int64_t n = N > G ? N : G;
     hipLaunchKernelGGL((k_shard_adopt<Real, NX, NZ, TK, OK>), dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                       s, (const Real*)rows, (Real*)x, N, Npad, rec, G, (const Real*)P, jitter, seed, rep, ep, pbase);
+                       s, (const Real*)rows, (Real*)x, N, Npad, rec, G, (const Real*)P, jitter, rp_jit, seed, rep, ep,
+                       pbase);
     return hipGetLastError();
   }
   static Ops make(int prec) {

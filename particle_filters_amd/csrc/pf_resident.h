@@ -770,12 +770,17 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const double ta1 = rec_aux ? row_sum_d(inr ? v5 : 0.0) : 0.0;
         const double ta2 = rec_aux ? row_sum_d(inr ? v6 : 0.0) : 0.0;
         if (lane < RF * RCOPIES) {  // RF granules x RCOPIES replicas, one sc1 store (the data is its own flag)
+          // the row reductions above left the record in row 0 (lanes 0..15): lane 0's values
+          // go to every lane, so lanes of all rows store correct replicas
           const int f = lane % RF, c = lane / RF;
-          const unsigned long long t0b = (unsigned long long)__double_as_longlong(t0);
-          const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(t0b >> 32)
-                             : f == 2 ? __float_as_uint(t00) : f == 3 ? __float_as_uint(t1)
-                             : f == 4 ? __float_as_uint(t2) : f == 5 ? __float_as_uint((float)ta1)
-                             : f == 6 ? __float_as_uint((float)ta2) : (unsigned)t0b;
+          const unsigned long long t0b = (unsigned long long)__double_as_longlong(uni(t0));
+          const unsigned pay = f == 0 ? __builtin_amdgcn_readfirstlane(__float_as_uint(Mt))
+                             : f == 1 ? (unsigned)(t0b >> 32)
+                             : f == 2 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t00))
+                             : f == 3 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t1))
+                             : f == 4 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t2))
+                             : f == 5 ? __float_as_uint((float)uni(ta1))
+                             : f == 6 ? __float_as_uint((float)uni(ta2)) : (unsigned)t0b;
           unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
           st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
         }

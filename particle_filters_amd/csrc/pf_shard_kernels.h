@@ -31,8 +31,8 @@ __global__ void __launch_bounds__(BLOCK) k_shard_offspring(const Real* __restric
 template <typename Real, int NX, int NZ, int TK, int OK>
 __global__ void __launch_bounds__(BLOCK) k_shard_adopt(const Real* __restrict__ rows, Real* __restrict__ x, int64_t N,
                                                        int64_t Npad, double* rec, int G, const Real* __restrict__ P,
-                                                       int jitter, uint64_t seed, uint32_t rep, uint32_t ep,
-                                                       int64_t pbase) {
+                                                       int jitter, const double* __restrict__ rp_jit, uint64_t seed,
+                                                       uint32_t rep, uint32_t ep, int64_t pbase) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(BLOCK) k_shard_adopt(const Real* __restrict__ 
     for (int d = 0; d < NX; ++d) v[d] = rows[i * NX + d];
     if (jitter) {
       Real nj[NX];
-      fill_normals<NX, Real>(seed, i, 0u, rep, ep, STREAM_JITTER, nullptr, N, nj, pbase);
+      fill_normals<NX, Real>(seed, i, 0u, rep, ep, STREAM_JITTER, rp_jit, N, nj, pbase);  // replay: [N][NX]
       M::add_lower(v, nj, P, M::L::LJ);
     }
 #pragma unroll

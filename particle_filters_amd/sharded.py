@@ -129,11 +129,13 @@ class HipShard:
             N._lib.pf_destroy(self._h)
         self._h = None
 
-    def initialize(self, mean, cov):
-        N.check(N.load().pf_initialize(self._h, N.dptr(mean), N.dptr(cov), None), "pf_initialize")
+    def initialize(self, mean, cov, replay=None):
+        rp = None if replay is None else np.ascontiguousarray(replay, dtype=float)
+        N.check(N.load().pf_initialize(self._h, N.dptr(mean), N.dptr(cov), N.dptr(rp)), "pf_initialize")
 
-    def predict(self, u):
-        N.check(N.load().pf_predict(self._h, N.dptr(u), None), "pf_predict")
+    def predict(self, u, replay=None):
+        rp = None if replay is None else np.ascontiguousarray(replay, dtype=float)
+        N.check(N.load().pf_predict(self._h, N.dptr(u), N.dptr(rp)), "pf_predict")
 
     def update(self, z, lse_prev):
         st = N.ShardStats()
@@ -149,11 +151,12 @@ class HipShard:
                                             N.C.c_void_p(self.outbox.data_ptr())), "pf_shard_offspring")
         return self.outbox[:n]
 
-    def adopt(self):
+    def adopt(self, jitter=None):
         mean = np.empty(self.nx)
         cov = np.empty((self.nx, self.nx))
-        N.check(N.load().pf_shard_adopt(self._h, N.C.c_void_p(self.inbox.data_ptr()), N.dptr(mean), N.dptr(cov)),
-                "pf_shard_adopt")
+        jp = None if jitter is None else np.ascontiguousarray(jitter, dtype=float)
+        N.check(N.load().pf_shard_adopt(self._h, N.C.c_void_p(self.inbox.data_ptr()), N.dptr(jp), N.dptr(mean),
+                                        N.dptr(cov)), "pf_shard_adopt")
         return mean, cov
 
     def sync_torch(self):
@@ -218,11 +221,18 @@ class ShardedParticleFilter:
     ``comm=None``: ``n_shards`` shards in this process (``devices`` cycles over the visible
     GPUs, default all on ``device``).  ``comm=DistComm()``: this rank's shard of a
     ``world``-rank filter on ``device``.  ``shard_factory`` builds one shard (default
-    :class:`HipShard`); the CPU tests substitute the NumPy shard of ``oracle/``."""
+    :class:`HipShard`); the CPU tests substitute the NumPy shard of ``oracle/``.
+
+    ``rng_mode="host"`` replays the reference's own draw stream (``rng``, a NumPy Generator
+    used exactly as pf.py:128,160,217,236 use it): every rank draws the full ``(Np, nx)``
+    normals / the systematic U and hands each shard its rows — the parity mode, pinned to the
+    reference's outputs (tests/test_gpu_sharded.py).  ``"device"`` draws Philox numbers of
+    the global particle indices on the shards."""
 
     def __init__(self, g, h, Q, R, *, Np: int, resample_thresh: float = 0.5, regularize_after_resample: bool = False,
                  seed: int = 0, precision: str = "fp32", comm: Optional[DistComm] = None, n_shards: int = 1,
-                 device: int = 0, devices: Optional[List[int]] = None, shard_factory=None):
+                 device: int = 0, devices: Optional[List[int]] = None, shard_factory=None, rng=None,
+                 rng_mode: str = "device"):
         if not M.is_device_model(g, h):
             raise NotImplementedError("ShardedParticleFilter needs particle_filters_amd.models g / h")
         self.g, self.h = g, h
@@ -234,8 +244,14 @@ class ShardedParticleFilter:
         self.regularize_after_resample = bool(regularize_after_resample)
         self.comm = comm
         self.W = comm.world if comm is not None else int(n_shards)
-        if self.Np % self.W or (self.Np // self.W) % 4:
-            raise ValueError("Np must be W * N_loc with N_loc a multiple of 4")
+        if rng_mode not in ("device", "host"):
+            raise ValueError("rng_mode must be 'device' or 'host'")
+        self.rng_mode = rng_mode
+        self.rng = np.random.default_rng() if rng is None else rng
+        if self.Np % self.W:
+            raise ValueError("Np must be W * N_loc")
+        if rng_mode == "device" and self.nx == 1 and (self.Np // self.W) % 4:
+            raise ValueError("device-RNG shards of a scalar state need N_loc % 4 == 0 (Philox groups of 4)")
         self.n_loc = self.Np // self.W
         self.mine = [comm.rank] if comm is not None else list(range(self.W))
         devs = devices or [device]
@@ -262,6 +278,16 @@ class ShardedParticleFilter:
         except Exception:
             pass
 
+    # ------------------------------------------------------------------ host replay
+    def _host_normals(self):
+        """The reference's (Np, nx) normal draw (pf.py:128, 217, 236), or None in device mode."""
+        if self.rng_mode != "host":
+            return None
+        return np.asarray(self.rng.standard_normal((self.Np, self.nx)), dtype=float)
+
+    def _rows(self, a, g):
+        return None if a is None else a[g * self.n_loc:(g + 1) * self.n_loc]
+
     # ------------------------------------------------------------------ collectives
     def _gather(self, rows: dict) -> Array:
         """per-shard vectors of every shard, in shard order."""
@@ -271,6 +297,8 @@ class ShardedParticleFilter:
         return self.comm.allgather(v, self.shards[r])
 
     def _resample(self, U: float, W: Array):
+        if self.rng_mode == "host":
+            U = float(self.rng.random())  # pf.py:160
         B = boundaries(W)
         a = slot_starts(B, U, self.Np)
         mass = np.diff(B)
@@ -301,9 +329,10 @@ class ShardedParticleFilter:
                     self.comm.sendrecv(send, dst, recv, src)
                 if hasattr(me, "sync_torch"):
                     me.sync_torch()
+        jit = self._host_normals() if self.regularize_after_resample else None  # pf.py:212-218
         stats = {}
         for g, s in self.shards.items():
-            m, c = s.adopt()
+            m, c = s.adopt(self._rows(jit, g))
             stats[g] = np.concatenate([m, c.ravel()])
         allst = self._gather(stats)
         means = allst[:, :self.nx]
@@ -318,8 +347,9 @@ class ShardedParticleFilter:
         """pf.py:110-132: particles ~ N(mean, cov + 1e-10 I) on every shard, uniform weights."""
         m = np.ascontiguousarray(np.asarray(mean, float).reshape(self.nx))
         c = np.ascontiguousarray(np.asarray(cov, float).reshape(self.nx, self.nx))
-        for s in self.shards.values():
-            s.initialize(m, c)
+        n0 = self._host_normals()
+        for g, s in self.shards.items():
+            s.initialize(m, c, self._rows(n0, g))
         self.t = 0
         self._lse_prev = 0.0
         self._neff = float(self.Np)
@@ -334,8 +364,9 @@ class ShardedParticleFilter:
         """pf.py:223-237."""
         self._need_init()
         uu = None if u is None else np.ascontiguousarray(np.asarray(u, float).reshape(self.nx))
-        for s in self.shards.values():
-            s.predict(uu)
+        n = self._host_normals()
+        for g, s in self.shards.items():
+            s.predict(uu, self._rows(n, g))
 
     def update(self, z) -> ShardedState:
         """pf.py:239-269 over all shards: global weights, Neff, decision, resample, moments."""

@@ -143,3 +143,31 @@ def test_two_processes_gloo_one_gpu(golden_sv):
         np.testing.assert_allclose(means, m2, rtol=0, atol=1e-12)
         np.testing.assert_allclose(neff, n2, rtol=1e-12)
     np.testing.assert_allclose(np.concatenate([o[4] for o in out]), x2, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name,W", [("sv_logsq_reg", 2), ("sv_logsq_reg", 4), ("sv_logsq", 4), ("l96", 2),
+                                    ("l96", 4)])
+def test_host_replay_device_shards_match_reference(name, W, golden_runs, golden_sv, golden_l96, golden_mat):
+    """The sharded engine against the REFERENCE (tests/golden/pf_runs.npz, made by importing
+    /root/reference/models/particle_filter.py): W fp64 device shards replaying the reference's
+    NumPy draw stream (each shard gets its rows of the initial / process / jitter normals, every
+    rank the systematic U) reproduce the run at test_replay_fp64_matches_reference's tolerances:
+    identical decisions, means rtol 1e-9, Neff rtol 1e-9, final particles 1e-9."""
+    from tests import pf_cases
+    ssm, Z, controls, kw = pf_cases.build(name, golden_sv, golden_l96, golden_mat, golden_runs)
+    ref = pf_cases.golden(golden_runs, name)
+    if name.startswith("sv_logsq"):
+        g, h = M.SVTransition(0.95), M.SVLogSqObservation(1.0)
+    else:
+        g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+    pf = SH.ShardedParticleFilter(g, h, ssm.Q, ssm.R, Np=kw["Np"], resample_thresh=kw["thresh"],
+                                  regularize_after_resample=kw["reg"], precision="fp64", n_shards=W,
+                                  rng_mode="host", rng=np.random.default_rng(kw["seed"]))
+    pf.initialize(np.asarray(kw["mean0"], float), np.asarray(kw["cov0"], float))
+    means, neff, flags = pf.run(Z)
+    parts = np.concatenate([pf.local_particles()[k] for k in range(W)])
+    pf.close()
+    assert np.array_equal(flags, ref["flags"]), f"{name} W={W}: resample decisions differ"
+    np.testing.assert_allclose(means, ref["means"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(neff, ref["neff"], rtol=1e-9)
+    np.testing.assert_allclose(parts, ref["final_particles"], rtol=1e-9, atol=1e-9)

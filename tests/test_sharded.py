@@ -143,3 +143,36 @@ def test_gloo_two_ranks_follow_one_shard():
         np.testing.assert_allclose(means, m1, rtol=0, atol=1e-10)
         np.testing.assert_allclose(neff, n1, rtol=1e-10)
     np.testing.assert_allclose(np.concatenate([o[4] for o in out]), x1, rtol=0, atol=1e-10)
+
+
+# ---------------------------------------------------------------------------
+# host replay of the reference's draw stream: the sharded filter against the
+# reference's own outputs (tests/golden/pf_runs.npz, /root/reference/models/
+# particle_filter.py:146-220 for the resample it shards)
+# ---------------------------------------------------------------------------
+def _sv_models(name):
+    if name.startswith("sv_logsq"):
+        return M.SVTransition(0.95), M.SVLogSqObservation(1.0)
+    return M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+
+
+@pytest.mark.parametrize("name,W", [("sv_logsq_reg", 2), ("sv_logsq_reg", 4), ("sv_logsq", 4), ("l96", 2),
+                                    ("l96", 4)])
+def test_host_replay_shards_match_reference(name, W, golden_runs, golden_sv, golden_l96, golden_mat):
+    """W NumPy shards (fp64) driven by the reference's NumPy draw stream reproduce the
+    reference's run: identical decisions, means / Neff within 1e-9 (the shard CDF segments are
+    rescaled pieces of the global CDF: ancestors agree except at exact ties)."""
+    from tests import pf_cases
+    ssm, Z, controls, kw = pf_cases.build(name, golden_sv, golden_l96, golden_mat, golden_runs)
+    ref = pf_cases.golden(golden_runs, name)
+    g, h = _sv_models(name)
+    pf = SH.ShardedParticleFilter(g, h, ssm.Q, ssm.R, Np=kw["Np"], resample_thresh=kw["thresh"],
+                                  regularize_after_resample=kw["reg"], n_shards=W, rng_mode="host",
+                                  rng=np.random.default_rng(kw["seed"]), shard_factory=shard_oracle.factory(ssm))
+    pf.initialize(np.asarray(kw["mean0"], float), np.asarray(kw["cov0"], float))
+    means, neff, flags = pf.run(Z)
+    assert np.array_equal(flags, ref["flags"])
+    np.testing.assert_allclose(means, ref["means"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(neff, ref["neff"], rtol=1e-9)
+    parts = np.concatenate([pf.local_particles()[s] for s in range(W)])
+    np.testing.assert_allclose(parts, ref["final_particles"], rtol=1e-9, atol=1e-9)
