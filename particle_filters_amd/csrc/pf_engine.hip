@@ -481,14 +481,23 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.regularize = h->regularize;
   q.r_diag = h->r_diag;
   q.rep_base = h->rep_base;
+  q.Rtot = h->R;
+  // Replicates are independent filters: when all R do not fit co-resident, groups of as many
+  // as fit run one after another (each replicate computes exactly what it computes alone, so
+  // the path - and every replicate's result - does not depend on R or on the sharding).
+  const int cap = h->ops->resident_cap ? h->ops->resident_cap() : 0;
+  const int Rg = cap >= G ? std::max(1, std::min(h->R, cap / G)) : h->R;
   if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
-  const hipError_t e = h->ops->resident(q, G, h->R, h->stream);
-  if (h->timing && e == hipSuccess) HIPCHK(hipEventRecord(h->tev[1], h->stream));
-  if (e == hipErrorCooperativeLaunchTooLarge) {
-    (void)hipGetLastError();
-    return PF_OK;  // not co-resident here: launch-per-step path
+  for (int r0 = 0; r0 < h->R; r0 += Rg) {
+    q.r0 = r0;
+    const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream);
+    if (e == hipErrorCooperativeLaunchTooLarge && r0 == 0) {
+      (void)hipGetLastError();
+      return PF_OK;  // not co-resident here: launch-per-step path
+    }
+    if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
   }
-  if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
+  if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   h->res_tag += (uint32_t)tag_span;
   h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;

@@ -34,6 +34,7 @@ struct Ops {
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
   // cannot be co-resident (the caller then runs the launch-per-step path).
   hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t);
+  int (*resident_cap)();  // workgroups of k_resident co-resident on the current device (0: unknown)
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
                                 double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t);
@@ -126,6 +127,7 @@ struct Launch {
     o.moments = &moments;
     o.prepare = &prepare;
     o.resident = nullptr;
+    o.resident_cap = nullptr;
     o.shard_offspring = &shard_offspring;
     o.shard_adopt = &shard_adopt;
     return o;
@@ -172,28 +174,35 @@ struct ResidentLaunch {
       void* args[] = {&q};
       return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
     }
+    if ((long long)G * R > (long long)cap()) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
+    return hipGetLastError();
+  }
+  // CUs x workgroups per CU from the occupancy API, cached per device
+  static int cap() {
     static int cached_dev = -1, cached_cap = 0;
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (dev != cached_dev) {
       int cus = 0, per_cu = 0;
-      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RBS, 0);
-      if (e != hipSuccess) return e;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_resident<float, NX, NZ, TK, OK>, RBS,
+                                                       0) != hipSuccess)
+        return 0;
       cached_dev = dev;
       cached_cap = cus * per_cu;
     }
-    if ((long long)G * R > (long long)cached_cap) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
-    return hipGetLastError();
+    return cached_cap;
   }
 };
 
 template <int NX, int NZ, int TK, int OK>
 inline void register_both() {
   Ops f32 = Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32);
-  if constexpr (NX == 1) f32.resident = &ResidentLaunch<NX, NZ, TK, OK>::launch;
+  if constexpr (NX == 1) {
+    f32.resident = &ResidentLaunch<NX, NZ, TK, OK>::launch;
+    f32.resident_cap = &ResidentLaunch<NX, NZ, TK, OK>::cap;
+  }
   register_ops(f32);
   register_ops(Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64));
 }

@@ -154,6 +154,7 @@ struct ResParams {
   // need no zeroing launch per launch (no memset in front of the kernel).
   uint32_t tag0;
   unsigned long long flag0;
+  int r0, Rtot;  // first replicate of this launch's group; the handle's replicate count (strides)
 };
 
 // Granules a verifying workgroup reads: every workgroup needs M, S0 (both words), S00
@@ -519,7 +520,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   __shared__ float4 snx[NSNAP][RPV * RBS];
   __shared__ float4 snl[NSNAP][RPV * RBS];
 
-  const int b = blockIdx.x, r = blockIdx.y, R = gridDim.y;
+  // replicate r of the handle's R: a launch covers replicates [r0, r0 + gridDim.y) (a group
+  // that fits co-resident; groups run one after another, each replicate is independent)
+  const int b = blockIdx.x, r = p.r0 + (int)blockIdx.y, R = p.Rtot;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t rep = (uint32_t)(r + p.rep_base);
   // model parameters, loaded once into registers (uniform; a few floats)

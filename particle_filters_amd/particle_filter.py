@@ -76,10 +76,17 @@ class _DeviceState(PFState):
     @particles.setter
     def particles(self, value) -> None:
         value = np.asarray(value, float)
-        object.__setattr__(self, "_particles", value)
         if self._fresh():
-            self._pf._upload_state(value, None if self._weights is None else self._weights)
+            # the weights stay what they are (pf.py keeps state.weights when particles are
+            # assigned): fetch them first unless the device says they are uniform
+            w = self._weights
+            if w is None and not N.load().pf_weights_uniform(self._pf._handle):
+                w = self.weights
+            object.__setattr__(self, "_particles", value)
+            self._pf._upload_state(value, w)
             object.__setattr__(self, "_version", self._pf._version)
+        else:
+            object.__setattr__(self, "_particles", value)
 
     @property
     def weights(self) -> Array:  # type: ignore[override]

@@ -160,3 +160,30 @@ def test_resident_bench_config(monkeypatch):
     print(f"N=1e6: RMSE resident {ra:.7f} launch-per-step {rb:.7f}; decisions agree {np.mean(a.flags == b.flags):.4f}")
     assert abs(ra - rb) <= 1e-4
     assert np.mean(a.flags == b.flags) >= 0.99
+
+
+def test_resident_replicate_groups_are_bitwise_single_replicates(golden_sv):
+    """R replicates whose grids do not all fit co-resident run as sequential groups of the
+    resident kernel: every replicate is bitwise the single-replicate run with the same Philox
+    replicate id (the path does not depend on R or on the multi-GPU sharding)."""
+    from particle_filters_amd import _native as NV
+    Z = np.log(golden_sv["Y0"][1:150] ** 2)[:, None]
+    kw = dict(Np=200_000, seed=31, resample_thresh=0.5)
+    big = ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]],
+                              n_replicates=8, **kw)  # 8 x 49 workgroups > 256 co-resident
+    big.initialize([0.0], [[0.5]])
+    rb = big.run(Z)
+    assert NV.load().pf_last_run_resident(big.handle)
+    for r in (0, 5, 7):
+        one = ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]],
+                                  n_replicates=1, replicate_base=r, **kw)
+        one.initialize([0.0], [[0.5]])
+        ro = one.run(Z)
+        assert NV.load().pf_last_run_resident(one.handle)
+        assert np.array_equal(ro.means[:, 0], rb.means[:, r])
+        assert np.array_equal(ro.neff[:, 0], rb.neff[:, r])
+        assert np.array_equal(ro.flags[:, 0], rb.flags[:, r])
+        assert np.array_equal(one.particles()[0], big.particles()[r])
+        one.close()
+    assert rb.flags.sum() >= 8
+    big.close()

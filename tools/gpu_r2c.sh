@@ -12,7 +12,7 @@ step() {  # step <name> <timeout> <cmd...>; exit status 0/1 go on, anything else
   echo "$name rc=$rc" | tee -a $D/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step t_new 600 python -u -m pytest tests/test_gpu_resident_oracle.py tests/test_gpu_sv_exact.py tests/test_gpu_sharded.py tests/test_gpu_distributed.py -v -s --timeout 300 --timeout-method thread
+step t_new 700 python -u -m pytest tests/test_gpu_resident_oracle.py tests/test_gpu_sv_exact.py tests/test_gpu_sharded.py tests/test_gpu_distributed.py tests/test_gpu_api_edges.py tests/test_gpu_resident.py -v -s --timeout 300 --timeout-method thread
 for k in 20 1000; do
   w=$((k / 10 > 5 ? k / 10 : 5))
   for v in rc1 rc4; do
