@@ -1203,7 +1203,7 @@ pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, d
     HIPCHK(hipMemcpyAsync(h->d_replay_b, jitter, (size_t)h->N * h->nx * sizeof(double), hipMemcpyHostToDevice,
                           h->stream));
     rj = h->d_replay_b;
-  } else if (h->ops->ch > 1 && h->pbase % 4) {
+  } else if (h->regularize && h->ops->ch > 1 && h->pbase % 4) {
     return fail(PF_E_ARG, "device-RNG jitter of a scalar-state shard needs N_loc % 4 == 0 (or host replay)");
   }
   HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, rj,

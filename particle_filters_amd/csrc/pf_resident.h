@@ -542,7 +542,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const unsigned long long* gbase0 = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
 #ifdef PF_STAMPS
-  const bool stamp_me = b == 0 && r == 0 && t == 0;
+#ifndef PF_STAMP_T
+#define PF_STAMP_T 0
+#endif
+  const bool stamp_me = b == 0 && r == 0 && t == PF_STAMP_T;  // PF_STAMP_T: the stamped thread (wave)
   unsigned long long racc[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) racc[k] = 0;
