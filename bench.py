@@ -20,6 +20,7 @@ Workloads (BASELINE.json configs; the default is the headline metric's config):
        8 replicates per GPU (64 over 8 GPUs)
   ledh config 5: LEDH particle flow on L96 d = 40, N = 1e4, 8 lambda steps (fp64)
   edh  config 5's job with the EDH global flow (EDH_particle_filter.py, RK4) (fp64)
+  ledh_mat  the MAT notebook's joint LEDH run: 16-D, 25 sensors, N = 500, L = 64, 39 steps (fp64)
 
 Extra JSON fields:
   roofline      dominant kernel.  SV: k_resident<f32, SV> — ONE launch runs all K
@@ -207,7 +208,7 @@ class MAT(Workload):
                 "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
 
 
-WORKLOADS = {"sv": SV, "sv64": SV64, "l96": L96, "mat": MAT, "ledh": None, "edh": None}
+WORKLOADS = {"sv": SV, "sv64": SV64, "l96": L96, "mat": MAT, "ledh": None, "edh": None, "ledh_mat": None}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector 157.3 TF of MI355X_MICROARCH.md)
 
 
@@ -224,9 +225,23 @@ def ledh_flops_per_particle(nx, nz, L):
     return rk4 + noise + y0 + L * per_lam + quad
 
 
-def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
+def ledh_pp_flops_per_particle(nx, nz, L):
+    """Algorithmic FP64 flops of one particle-step of the per-particle LEDH flow in the
+    reference's formulation (LEDH_particle_filter.py:136-179): per lambda step P H^T
+    (2 nx^2 nz), S = lam H P H^T + R (2 nz^2 nx), its factorisation and the solve for
+    S^-1 H ((2/3) nz^3 + 2 nz^2 nx), A = -1/2 P H^T S^-1 H (2 nx^2 nz), b and the
+    eta update (~10 nx^2), slogdet(I + dlam A) ((2/3) nx^3)."""
+    per_lam = 4 * nx * nx * nz + 4 * nz * nz * nx + (2 * nz ** 3) // 3 + (2 * nx ** 3) // 3 + 10 * nx * nx
+    return L * per_lam
+
+
+def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"):
     """BASELINE config 5: LEDH particle flow on Lorenz-96 d = 40, N = 1e4, 8 lambda steps
-    (algo="edh": the same job with the EDH global flow of EDH_particle_filter.py, RK4 integrator)."""
+    (algo="edh": the same job with the EDH global flow of EDH_particle_filter.py, RK4 integrator).
+    model="mat": the reference's one published LEDH run — joint 4-target acoustic tracking
+    (16-D state, 25 sensors), N = 500, 64 lambda steps, 39 filter steps over the 40-step
+    scenario, 2095.74 s in the reference notebook
+    (PF_PF_results_reproduction_multi_target_acoustic_tracking.ipynb:1095, cells 5-6)."""
     import torch
 
     torch.cuda.set_device(local)
@@ -237,14 +252,30 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from particle_filters_amd import edh as ED, ledh as LD, models as M, simulators as S, trackers as TR
 
-    K = args.steps if args.steps is not None else 200
-    W = args.warmup if args.warmup is not None else 20
-    Np, L, nx, nz = 10_000, 8, 40, 10
-    sim = S.simulate_lorenz96(nx=40, F=8.0, dt=0.01, spinup_steps=1000, total_steps=W + K, Np=1, obs_interval=1,
-                              obs_fraction=4, obs_error_std=1.0, seed=42)
-    g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(sim.H_idx, 40)
-    Q, R = 0.1 ** 2 * np.eye(40), sim.R
-    mean0, cov0 = sim.ensemble_traj[0, 0], 2.0 * np.eye(40)
+    if model == "mat":
+        K = args.steps if args.steps is not None else 39
+        W = args.warmup if args.warmup is not None else 3
+        Np, L, nx, nz = 500, 64, 16, 25
+        cfg_s = S.ScenarioConfig(n_targets=4, n_steps=max(40, W + K + 1), sensor_grid_shape=(5, 5), psi=10.0, d0=0.1,
+                                 seed=56, use_article_init=True)
+        data = S.simulate_acoustic_dataset(cfg_s, S.DynamicsConfig())
+        g, h = M.CVTransition(4, 1.0), M.AcousticObservation(data["S"], 10.0, 0.1, 4)
+        Q, R = np.kron(np.eye(4), S.article_process_noise_cov()), 0.1 ** 2 * np.eye(25)
+        Xt = data["X"].reshape(data["X"].shape[0], 16)
+        # the notebook's joint prior: per-target N(mean, diag(10^2, 10^2, 1, 1)) around the start
+        mean0 = Xt[0] + np.tile([1.5, -1.0, 0.1, -0.1], 4)
+        cov0 = np.kron(np.eye(4), np.diag([100.0, 100.0, 1.0, 1.0]))
+        Zs, truth_all = data["Z"], Xt
+    else:
+        K = args.steps if args.steps is not None else 200
+        W = args.warmup if args.warmup is not None else 20
+        Np, L, nx, nz = 10_000, 8, 40, 10
+        sim = S.simulate_lorenz96(nx=40, F=8.0, dt=0.01, spinup_steps=1000, total_steps=W + K, Np=1, obs_interval=1,
+                                  obs_fraction=4, obs_error_std=1.0, seed=42)
+        g, h = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(sim.H_idx, 40)
+        Q, R = 0.1 ** 2 * np.eye(40), sim.R
+        mean0, cov0 = sim.ensemble_traj[0, 0], 2.0 * np.eye(40)
+        Zs, truth_all = sim.observations, sim.truth_traj
 
     def make():
         ekf = TR.ExtendedKalmanFilter(g, h, Q, R, jac_g=g.jacobian, jac_h=h.jacobian)
@@ -258,7 +289,7 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
                             rng=np.random.default_rng(42 + rank))
         return LD.LEDHFlowPF(*args_, cfg, rng_mode="device"), tracker
 
-    Z = sim.observations[1:]
+    Z = Zs[1:]
     pf, tracker = make()
     st = pf.init_from_gaussian(mean0, cov0)
     pf.run(st, Z[:max(W, 1)], tracker="device")  # warm-up (same sequence as the timed run)
@@ -297,16 +328,33 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
     t_host_total = time.perf_counter() - h0
     pf2.close()
     dev_s = elapsed
-    rmse = res.rmse(sim.truth_traj[W + 1:W + K + 1])
-    flops = ledh_flops_per_particle(nx, nz, L) * Np * K
+    rmse = res.rmse(truth_all[W + 1:W + K + 1])
+    per_particle = pf.shared_jacobian_path is False
+    fpp = ledh_pp_flops_per_particle(nx, nz, L) if per_particle else ledh_flops_per_particle(nx, nz, L)
+    flops = fpp * Np * K
+    if model == "mat":
+        wl_name = "joint 4-target acoustic tracking (16-D state, 25 sensors)"
+        data_desc = ("synthetic (simulate_acoustic_dataset 4 targets 5x5 sensors psi=10 d0=0.1 seed=56 article init; "
+                     "R=0.01 I, Q=blockdiag(article_process_noise_cov))")
+        notes = (f"N={Np} particles, {L} lambda steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
+                 "(analytic acoustic Jacobian), per-particle LEDH flow (pf_ledh_kernels.h k_flow_wave), Philox noise")
+    else:
+        wl_name = "L96 d=40"
+        data_desc = "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)"
+        notes = ("N=1e4 particles, 8 lambda steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
+                 "(analytic RK4 Jacobian), Philox process noise")
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             from oracle import edh_oracle as EO, ledh_oracle as LO
 
-            om = LO.lorenz96(40)
+            if model == "mat":
+                om = LO.acoustic_joint(h.S, psi=10.0, d0=0.1, n_targets=4, Q_single=S.article_process_noise_cov())
+                n_cpu = 100
+            else:
+                om = LO.lorenz96(40)
+                n_cpu = 1000
             steps = int(os.environ.get("PF_CPU_BASELINE_STEPS", "1"))
-            n_cpu = 1000
             tr = LO.make_ekf_tracker(om, mean0, cov0)
             if algo == "edh":
                 opf = EO.EDHOracle(tr, om, n_particles=n_cpu, n_lambda_steps=L, resample_ess_ratio=0.5,
@@ -321,21 +369,20 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
                 ost = opf.step(ost, Z[t], process_noise_sampler=sampler)
             cdt = time.perf_counter() - c0
             cpu = {"value": n_cpu * steps / cdt, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                   "sample": f"{algo.upper()} L96 d=40, N={n_cpu}, L={L}, {steps} step(s), faithful per-particle "
+                   "sample": f"{algo.upper()} {wl_name}, N={n_cpu}, L={L}, {steps} step(s), faithful per-particle "
                              f"restatement (oracle/{algo}_oracle.py, bit-identical to the reference "
                              f"{algo.upper()}FlowPF), {cdt:.1f} s",
                    "cores_on_host": os.cpu_count()}
         line = {
-            "metric": f"particle-steps/sec (N×T/s), {algo.upper()} flow filter L96 d=40",
+            "metric": f"particle-steps/sec (N×T/s), {algo.upper()} flow filter {wl_name}",
             "value": Np * K * world / elapsed, "unit": "particle-steps/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": elapsed * 1e3 / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)",
-            "config": {"workload": ("LEDH particle-flow PF (BASELINE config 5)" if algo == "ledh" else
-                                    "EDH particle-flow PF (config 5's job with the global EDH flow, RK4)") +
-                                   ": L96 d=40, N=1e4 particles, 8 lambda "
-                                   "steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
-                                   "(analytic RK4 Jacobian), Philox process noise",
+            "data": data_desc,
+            "config": {"workload": (("LEDH particle-flow PF" + (" (BASELINE config 5)" if model == "l96" else
+                                                                  " (the MAT notebook's joint LEDH run)"))
+                                    if algo == "ledh" else
+                                    "EDH particle-flow PF (the global EDH flow, RK4)") + f": {wl_name}, " + notes,
                        "n_particles": Np, "n_lambda": L, "shared_jacobian_path": pf.shared_jacobian_path,
                        "parallelism": f"replicas x{world} (one independent filter per GPU)"},
             "rmse": rmse, "resample_rate": float(np.mean(res.flags)),
@@ -343,12 +390,22 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False):
                                      "note": "EKF stepped on the host in NumPy, covariances uploaded, same device loop"},
             "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
-                         "kernel": ("whole LEDH job: k_ekf_seq + k_setup/k_compose" if algo == "ledh" else
-                                    "whole EDH job: k_ekf_seq + k_edh_setup") +
-                                   " + per step k_flow_affine, k_weights_small, k_gather, k_mom_part, k_mom_final",
-                         "flops_per_particle_step": ledh_flops_per_particle(nx, nz, L)},
+                         "kernel": ("whole LEDH job: k_ekf_seq + " + ("per step k_flow_wave (per-particle flow)"
+                                                                      if per_particle else
+                                                                      "k_setup/k_compose + per step k_ledh_fused"))
+                                   if algo == "ledh" else "whole EDH job: k_ekf_seq + k_edh_setup + per step k_ledh_fused",
+                         "flops_per_particle_step": fpp,
+                         "flops_note": "the reference formulation's per-particle dense algebra (estimate)"
+                                       if per_particle else "shared-Jacobian flow (see ledh_flops_per_particle)"},
             "cpu_baseline": cpu,
         }
+        if model == "mat" and algo == "ledh":
+            ref_s = 2095.74  # PF_PF_results_reproduction_multi_target_acoustic_tracking.ipynb:1095 (N=500, 39 steps)
+            line["reference_published"] = {
+                "value": 500 * 39 / ref_s, "unit": "particle-steps/s", "seconds": ref_s,
+                "source": "PF_PF_results_reproduction_multi_target_acoustic_tracking.ipynb:1095 (joint LEDH, N=500, "
+                          "L=64, 39 steps; reference NumPy on the authors' machine)",
+                "speedup": (Np * K * world / elapsed) / (500 * 39 / ref_s)}
         print(json.dumps(line), flush=True)
     pf.close()
     if dist:
@@ -487,8 +544,10 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     # a launcher (torchrun or spawn_ranks) sets WORLD_SIZE: then the RCCL group exists even at world 1
     use_dist = "WORLD_SIZE" in os.environ
-    if args.workload in ("ledh", "edh"):
-        return main_ledh(args, world, rank, local, algo=args.workload, use_dist=use_dist)
+    if args.workload in ("ledh", "edh", "ledh_mat"):
+        algo = "ledh" if args.workload == "ledh_mat" else args.workload
+        return main_ledh(args, world, rank, local, algo=algo, use_dist=use_dist,
+                         model="mat" if args.workload == "ledh_mat" else "l96")
     wl = WORKLOADS[args.workload]()
     K = args.steps if args.steps is not None else wl.defaults[0]
     W = args.warmup if args.warmup is not None else wl.defaults[1]

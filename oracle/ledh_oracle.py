@@ -307,6 +307,66 @@ def acoustic_single(S, psi=10.0, d0=0.1, Q=None, R=None) -> LEDHModel:
                           jac_g=lambda x, u: F)
 
 
+def acoustic_joint(S, psi=10.0, d0=0.1, n_targets=4, Q_single=None, R=None) -> LEDHModel:
+    """Joint multi-target acoustic wiring of the MAT notebook (PF_PF_results_reproduction_
+    multi_target_acoustic_tracking.ipynb cell 5: ``g_joint`` = CV per [x, y, vx, vy] block,
+    ``h_joint`` = sum over targets of psi/(|p_c - s|^2 + d0), ``jac_h_joint`` = per-target
+    blocks, ``Q_joint = blockdiag(Q_filter)``, ``R = 0.1^2 I``)."""
+    S = np.asarray(S, float)
+    ns, C = S.shape[0], int(n_targets)
+    nx = 4 * C
+    F1 = np.array([[1.0, 0.0, 1.0, 0.0], [0.0, 1.0, 0.0, 1.0], [0.0, 0.0, 1.0, 0.0], [0.0, 0.0, 0.0, 1.0]])
+    F = np.kron(np.eye(C), F1)
+    if Q_single is None:
+        Q_single = np.array([[3.0, 0.0, 0.1, 0.0], [0.0, 3.0, 0.0, 0.1], [0.1, 0.0, 0.03, 0.0],
+                             [0.0, 0.1, 0.0, 0.03]])
+    Q = np.kron(np.eye(C), np.asarray(Q_single, float))
+    if R is None:
+        R = 0.1 ** 2 * np.eye(ns)
+
+    def h(x):
+        z = np.zeros(ns)
+        for c in range(C):
+            pos = x[4 * c:4 * c + 2]
+            zc = np.zeros(ns)
+            for s in range(ns):
+                zc[s] = psi / (np.sum((pos - S[s]) ** 2) + d0)
+            z += zc
+        return z
+
+    def jac(x):
+        H = np.zeros((ns, nx))
+        for c in range(C):
+            pos = x[4 * c:4 * c + 2]
+            for s in range(ns):
+                diff = pos - S[s]
+                denom = (np.sum(diff ** 2) + d0) ** 2
+                H[s, 4 * c] = -2.0 * psi * diff[0] / denom
+                H[s, 4 * c + 1] = -2.0 * psi * diff[1] / denom
+        return H
+
+    def h_vec(X):
+        z = np.zeros((X.shape[0], ns))
+        for c in range(C):
+            dx = X[:, 4 * c, None] - S[None, :, 0]
+            dy = X[:, 4 * c + 1, None] - S[None, :, 1]
+            z = z + psi / ((dx ** 2 + dy ** 2) + d0)
+        return z
+
+    def jac_vec(X):
+        H = np.zeros((X.shape[0], ns, nx))
+        for c in range(C):
+            dx = X[:, 4 * c, None] - S[None, :, 0]
+            dy = X[:, 4 * c + 1, None] - S[None, :, 1]
+            den = ((dx ** 2 + dy ** 2) + d0) ** 2
+            H[:, :, 4 * c] = -2.0 * psi * dx / den
+            H[:, :, 4 * c + 1] = -2.0 * psi * dy / den
+        return H
+
+    return gaussian_model(nx, ns, Q, R, lambda x, u: F @ x, h, jac, lambda X, u: X @ F.T, h_vec, jac_vec,
+                          jac_g=lambda x, u: F)
+
+
 def lorenz96(nx=40, F=8.0, dt=0.01, obs_fraction=4, obs_error_std=1.0, q_std=0.1) -> LEDHModel:
     """L96 LEDH wiring (BASELINE config 5): g = one RK4 step + v, h = x[H_idx], constant
     selection Jacobian, Q = q_std^2 I (the build's choice, as for the SIR config 3)."""

@@ -132,6 +132,15 @@ def main():
     runs["acoustic"] = dict(model=LO.acoustic_single(S2, psi=float(mat["meta2"][2]), d0=float(mat["meta2"][3])),
                             Z=mat["Z2"][1:7], mean0=mat["X2"][0, 0], cov0=np.diag([100.0, 100.0, 1.0, 1.0]),
                             n_particles=100, n_lambda=3, ratio=0.5, seed=100)
+    # joint 4-target acoustic tracking, 16-D state, 5x5 sensors (the MAT notebook's h_joint wiring, the
+    # reference's only published LEDH run: PF_PF_results_reproduction_multi_target_acoustic_tracking.ipynb)
+    from simulator.simulator_Multi_acoustic_tracking import article_process_noise_cov  # reference
+    Xj = mat["X"]
+    m0 = Xj[0].reshape(-1) + np.tile([1.5, -1.0, 0.1, -0.1], Xj.shape[1])
+    runs["mat_joint"] = dict(model=LO.acoustic_joint(mat["S"], psi=float(mat["meta"][2]), d0=float(mat["meta"][3]),
+                                                     n_targets=Xj.shape[1], Q_single=article_process_noise_cov()),
+                             Z=mat["Z"][1:5], mean0=m0, cov0=np.kron(np.eye(Xj.shape[1]), np.diag([100.0, 100.0, 1.0, 1.0])),
+                             n_particles=96, n_lambda=8, ratio=0.5, seed=56)
     # Lorenz-96 d=40 (BASELINE config 5 wiring), short
     l96 = np.load(os.path.join(HERE, "l96_data.npz"))
     runs["l96"] = dict(model=LO.lorenz96(40), Z=l96["obs"][1:5], mean0=l96["ensemble"][0, 0], cov0=2.0 * np.eye(40),

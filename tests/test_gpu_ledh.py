@@ -51,6 +51,11 @@ def case(name):
     elif name == "l96":
         om = LO.lorenz96(40)
         gm, hm = M.L96Transition(8.0, 0.01, 40), M.SelectObservation(np.arange(0, 40, 4), 40)
+    elif name == "mat_joint":  # the MAT notebook's joint 16-D / 25-sensor wiring (nz = 25, per-particle flow)
+        from particle_filters_amd.simulators import article_process_noise_cov
+        pj, dj = float(MAT["meta"][2]), float(MAT["meta"][3])
+        om = LO.acoustic_joint(MAT["S"], psi=pj, d0=dj, n_targets=4, Q_single=article_process_noise_cov())
+        gm, hm = M.CVTransition(4, 1.0), M.AcousticObservation(MAT["S"], pj, dj, 4)
     else:
         raise KeyError(name)
     return om, gm, hm, g

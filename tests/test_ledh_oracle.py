@@ -13,6 +13,8 @@ import pytest
 
 from oracle import ledh_oracle as LO
 
+from particle_filters_amd.simulators import article_process_noise_cov  # noqa: E402  (restated, pinned)
+
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ledh_runs.npz"))
 NAMES = [str(n) for n in GOLD["names"]]
 
@@ -27,6 +29,8 @@ def case(name):
         "sv_exp": lambda: LO.sv_exp_half(0.95, 0.2, 1.0, 0.1),
         "acoustic": lambda: LO.acoustic_single(mat["S2"], psi=float(mat["meta2"][2]), d0=float(mat["meta2"][3])),
         "l96": lambda: LO.lorenz96(40),
+        "mat_joint": lambda: LO.acoustic_joint(mat["S"], psi=float(mat["meta"][2]), d0=float(mat["meta"][3]),
+                                               n_targets=4, Q_single=article_process_noise_cov()),
     }[name]()
     del sv
     return model, g

@@ -13,7 +13,7 @@ step() {  # step <name> <timeout> <cmd...>; exit status 0/1 go on, anything else
   echo "$name rc=$rc" | tee -a $D/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step t_new 700 python -u -m pytest tests/test_gpu_resident_oracle.py tests/test_gpu_sv_exact.py tests/test_gpu_sharded.py -v -s --timeout 300 --timeout-method thread
+step t_new 900 python -u -m pytest tests/test_gpu_resident_oracle.py tests/test_gpu_sv_exact.py tests/test_gpu_sharded.py tests/test_gpu_ledh.py -v -s --timeout 300 --timeout-method thread
 for v in st0 st7; do
   for T in 20 1000; do
     step stamps_${v}_T$T 200 env PF_COOP=0 PF_LIB=build/libpf_hip_$v.so python -u tools/diag_resident_stamps.py 1000000 $T
@@ -25,4 +25,5 @@ for k in 20 1000; do
     step b_${v}_k$k 300 env PF_COOP=0 PF_LIB=build/libpf_hip_$v.so python -u bench.py --steps $k --warmup $w --no-cpu-baseline --no-ref
   done
 done
+step b_ledh_mat 600 python -u bench.py --workload ledh_mat
 echo done >> $D/steps.log
