@@ -25,5 +25,10 @@ for k in 20 1000; do
     step b_${v}_k$k 300 env PF_COOP=0 PF_LIB=build/libpf_hip_$v.so python -u bench.py --steps $k --warmup $w --no-cpu-baseline --no-ref
   done
 done
+for c in 0 1; do
+  for T in 20 1000; do
+    step launch_coop${c}_T$T 200 env PF_COOP=$c python -u tools/diag_launch_overhead.py $T 20
+  done
+done
 step b_ledh_mat 600 python -u bench.py --workload ledh_mat
 echo done >> $D/steps.log
