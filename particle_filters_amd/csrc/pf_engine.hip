@@ -139,6 +139,14 @@ struct pf_handle {
   int64_t pbase = 0, n_total = 0;
   uint32_t shard_cdf_ep = 0;
   bool needs_cdf() const { return method == 1 || sys_cdf || sharded; }
+  // large-state systematic path: the update launch leaves the in-tile CDF prefix (StepParams::
+  // lcum_out) and the next gather reads it, so no k_cdf launch (lcum_valid: the current
+  // weights' prefix exists; set_state / gather-only launches invalidate it)
+  bool lcum_mode = false;
+  double* lcum[2] = {nullptr, nullptr};
+  int clcum = 0;
+  bool lcum_valid = false;
+  bool cdf_needed() const { return needs_cdf() && !(lcum_mode && lcum_valid && method == 0 && !sharded); }
   // per-step replicate heads (k_head, StepParams::head): -1 auto, 0 off, 1 on (PF_HEAD)
   int head_mode = -1;
   double* head = nullptr;  // [R][HEAD_STRIDE]
@@ -305,8 +313,14 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
   p.lw_out = h->lw[h->clw ^ 1];
   p.rec_in = h->rec[h->crec];
   p.rec_out = h->rec[h->crec ^ 1];
+  const bool use_lcum = h->lcum_mode && !h->sharded && h->method == 0;
+  p.lcum_in = (use_lcum && h->lcum_valid && p.allow_gather) ? h->lcum[h->clcum] : nullptr;
+  p.lcum_out = (use_lcum && p.do_update) ? h->lcum[h->clcum ^ 1] : nullptr;
   dim3 grid((unsigned)h->G, (unsigned)h->R);
   HIPCHK(h->ops->step(p, grid, step_lds(h, p.allow_gather != 0), h->stream));
+  if (p.lcum_out) h->clcum ^= 1;
+  // the prefix describes exactly the weights an update launch wrote
+  if (writes_lw || p.allow_gather) h->lcum_valid = p.lcum_out != nullptr;
   h->head_valid = false;  // the heads describe records this launch may have replaced
   if (writes_x) h->cx ^= 1;
   if (writes_lw) h->clw ^= 1;
@@ -388,7 +402,7 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
   p.cdf = h->cdf;
   p.allow_gather = 1;
   p.ep_resample = h->ep_res;
-  if (h->needs_cdf()) {
+  if (h->cdf_needed()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -677,6 +691,14 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   }
   if (h->needs_cdf() && hipMalloc((void**)&h->cdf, (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of cdf failed"));
+  {
+    const char* le = std::getenv("PF_LCUM");  // PF_LCUM=0: materialise the CDF with k_cdf (A/B)
+    h->lcum_mode = h->sys_cdf && !(le && le[0] == '0');
+  }
+  if (h->lcum_mode)
+    for (int k = 0; k < 2; ++k)
+      if (hipMalloc((void**)&h->lcum[k], (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
+        return cleanup(fail(PF_E_HIP, "hipMalloc of the CDF prefix failed"));
   if (const char* he = std::getenv("PF_HEAD")) h->head_mode = std::atoi(he) != 0 ? 1 : 0;
   if (hipMalloc((void**)&h->head, (size_t)h->R * HEAD_STRIDE * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of replicate heads failed"));
@@ -702,6 +724,8 @@ void pf_destroy(pf_handle* h) {
   for (hipEvent_t e : h->tev)
     if (e) (void)hipEventDestroy(e);
   if (h->head) (void)hipFree(h->head);
+  for (double* q : h->lcum)
+    if (q) (void)hipFree(q);
   for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif})
     if (p) (void)hipFree(p);
@@ -746,6 +770,7 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   if (st) return st;
   h->initialized = true;
   h->pending = false;
+  h->lcum_valid = false;
   return PF_OK;
 }
 
@@ -771,7 +796,7 @@ pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
   }
   // a resample decided but not yet applied is fused into this launch
   const bool gather = h->pending;
-  if (gather && h->needs_cdf()) {
+  if (gather && h->cdf_needed()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -916,7 +941,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     p.ep_resample = prev_res;
     p.out_step = s >= 1 ? s - 1 : -1;
     p.out_post_step = s >= 2 ? s - 2 : -1;
-    if (gather_possible && h->needs_cdf()) {
+    if (gather_possible && h->cdf_needed()) {
       pf_status st = launch_cdf(h, p);
       if (st) return st;
     }
@@ -935,7 +960,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   p.ep_resample = prev_res;
   p.out_step = T - 1;
   p.out_post_step = T >= 2 ? T - 2 : -1;
-  if (h->needs_cdf()) {
+  if (h->cdf_needed()) {
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
@@ -1266,6 +1291,7 @@ pf_status pf_set_state(pf_handle* h, const double* particles, const double* weig
         soa[((size_t)r * nx + d) * h->Npad + i] = particles[((size_t)r * h->N + i) * nx + d];
   pf_status st = upload_real(h, h->x[h->cx], soa.data(), soa.size());
   if (st) return st;
+  h->lcum_valid = false;  // uploaded weights: k_cdf materialises their CDF when a resample needs it
   // records: one tile carrying S0 = 1 at m = 0 (so lse = 0), the rest empty; or uniform
   std::vector<double> rec((size_t)R * h->G * h->ops->rec_size, 0.0);
   const size_t G = (size_t)h->G;
@@ -1424,7 +1450,7 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
     p.ep_resample = prev_res;
     p.out_step = s >= 1 ? s - 1 : -1;
     p.out_post_step = s >= 2 ? s - 2 : -1;
-    if (gather_possible && h->needs_cdf()) st = launch_cdf(h, p);
+    if (gather_possible && h->cdf_needed()) st = launch_cdf(h, p);
     if (!st) {
       (void)hipEventRecord(ev[s], h->stream);
       st = launch_step(h, p, true, true, true);
@@ -1442,7 +1468,7 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
     q.allow_gather = 1;
     q.ep_resample = prev_res;
     q.cdf = h->cdf;
-    if (h->needs_cdf()) st = launch_cdf(h, q);
+    if (h->cdf_needed()) st = launch_cdf(h, q);
     if (!st) st = launch_step(h, q, true, false, true);
   }
   (void)hipStreamSynchronize(h->stream);

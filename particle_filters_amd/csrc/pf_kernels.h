@@ -220,6 +220,12 @@ struct StepParams {
   int rep_base;           // global id of replicate 0 of this launch (Philox counter word)
   int lq_local, lj_local; // chol(Q) / jitter factor block-diagonal in the lane blocks of k_step_grp
   int sys_cdf;            // systematic ancestors searched in the materialised CDF `cdf` (k_step_grp)
+  // k_step_grp, systematic: the in-tile inclusive prefix sum_{j' <= j} e^(l_j' - m_k) of the weights
+  // in rec_in, written by the launch that produced them (lcum_out, tile_cdf's summation order) and
+  // read by the next gather (lcum_in) as cdf[j] = P_k + c_k lcum[j] — tile_cdf's values without the
+  // k_cdf launch.  Null: not available (k_cdf materialises `cdf` instead).
+  const double* lcum_in;
+  double* lcum_out;
   // within-filter sharding (pf_shard.h): global index of local particle 0 (Philox counters) and
   // the global log normaliser of the previous weights (replaces the local one when use_lse_ext)
   int64_t pbase;

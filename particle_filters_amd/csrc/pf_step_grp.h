@@ -425,7 +425,15 @@ k_step_grp(StepParams p) {
       // k_cdf materialised (tile_cdf arithmetic: the same ancestors as the per-tile path below).
       // The source tiles of this block's (monotone) positions are staged in LDS when they are few.
       const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
-      const double* C = p.cdf + (int64_t)r * p.N;
+      // the CDF: materialised by k_cdf (C), or built on the fly from the in-tile prefix the
+      // previous launch left (L): cdf[j] = P_k + c_k L[j], c_k = e^(m_k - M) / S (tile_cdf's
+      // arithmetic, so both give the same doubles)
+      const double* C = p.lcum_in ? nullptr : p.cdf + (int64_t)r * p.N;
+      const double* Lc = p.lcum_in ? p.lcum_in + (int64_t)r * p.N : nullptr;
+      auto ck = [&](int k) {
+        const double mk = rec_in[RC::M * p.G + k];
+        return (mk > -INFINITY) ? exp(mk - h.M) / h.Sscan : 0.0;
+      };
       __shared__ int krange[2];
       if (t == 0) {
         krange[0] = prefix_tile(Pl, p.G, (U + (double)o0) / (double)p.N);
@@ -438,7 +446,12 @@ k_step_grp(StepParams p) {
       if (staged)
         for (int e = t; e < nk * p.tile; e += BS) {
           const int64_t g = (int64_t)klo * p.tile + e;
-          stg[e] = g < p.N ? C[g] : INFINITY;
+          if (Lc) {
+            const int k = klo + e / p.tile;
+            stg[e] = g < p.N ? Pl[k] + ck(k) * Lc[g] : INFINITY;
+          } else {
+            stg[e] = g < p.N ? C[g] : INFINITY;
+          }
         }
       __syncthreads();
       for (int c = t; c < nchunks; c += BS) {  // every lane takes a slot (independent searches)
@@ -452,6 +465,12 @@ k_step_grp(StepParams p) {
             while (lo < hi) {
               const int mid = (lo + hi) >> 1;
               if (pos < cs[mid]) hi = mid; else lo = mid + 1;
+            }
+          } else if (Lc) {
+            const double bk = Pl[k], cc = ck(k);
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (pos < bk + cc * Lc[s0 + mid]) hi = mid; else lo = mid + 1;
             }
           } else {
             while (lo < hi) {
@@ -621,6 +640,30 @@ k_step_grp(StepParams p) {
   __syncthreads();
   PF_STAMP(5);
   for (int k = t; k < RC::SIZE; k += BS) rec_out[k * p.G + b] = fin[k];
+  if (p.lcum_out && p.do_update) {
+    // the in-tile prefix of the new weights, exactly as tile_cdf (k_cdf) sums them: thread t owns
+    // the contiguous elements [t per, t per + per), block exclusive scan, then the running sum.
+    // lw_out of this tile was written above by this workgroup (visible after the barrier).
+    const int64_t s0 = o0;
+    const int len = nchunks;
+    const int per = (len + BS - 1) / BS;
+    const int j0 = t * per;
+    const double mk = fin[RC::M];
+    const Real m = (Real)mk;
+    double accs = 0.0;
+    for (int j = j0; j < j0 + per && j < len; ++j) {
+      const Real l = lw_out[s0 + j];
+      accs += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
+    }
+    double tot;
+    double off = block_excl_scan<BS>(accs, red, &tot);
+    double* Lo = p.lcum_out + (int64_t)r * p.N + s0;
+    for (int j = j0; j < j0 + per && j < len; ++j) {
+      const Real l = lw_out[s0 + j];
+      off += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
+      Lo[j] = off;
+    }
+  }
 }
 
 }  // namespace pf

@@ -13,7 +13,7 @@ step() {  # step <name> <timeout> <cmd...>; exit status 0/1 go on, anything else
   echo "$name rc=$rc" | tee -a $D/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step t_new 900 python -u -m pytest tests/test_gpu_resident_oracle.py tests/test_gpu_sv_exact.py tests/test_gpu_sharded.py tests/test_gpu_ledh.py -v -s --timeout 300 --timeout-method thread
+step t_gpu 1200 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread
 for v in st0 st7; do
   for T in 20 1000; do
     step stamps_${v}_T$T 200 env PF_COOP=0 PF_LIB=build/libpf_hip_$v.so python -u tools/diag_resident_stamps.py 1000000 $T
@@ -24,6 +24,9 @@ for k in 20 1000; do
   for v in abl1 abl2; do
     step b_${v}_k$k 300 env PF_COOP=0 PF_LIB=build/libpf_hip_$v.so python -u bench.py --steps $k --warmup $w --no-cpu-baseline --no-ref
   done
+done
+for lc in 0 1; do
+  step b_l96_lcum$lc 300 env PF_LCUM=$lc python -u bench.py --workload l96 --steps 100 --warmup 10 --no-cpu-baseline --no-ref
 done
 for c in 0 1; do
   for T in 20 1000; do
