@@ -477,10 +477,9 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
   h->L = std::max(1, (int)o->n_lambda);                   // ledh.py:132
   h->algo = algo;
   h->integ = integ;
-  if (algo == 0 && (size_t)h->L * (size_t)(nx * nz + nz * nz + nx + nz + 1) * 8 > 120 * 1024) {
-    delete h;
-    return lfail(PF_E_ARG, "n_lambda_steps too large for the staged flow table of this model");
-  }
+  // the shared-Jacobian path stages its whole flow table in LDS; past that size (many lambda
+  // steps) a linear h takes the per-particle flow instead (the same flow, particle by particle)
+  const bool table_fits = (size_t)h->L * (size_t)(nx * nz + nz * nz + nx + nz + 1) * 8 <= 120 * 1024;
   h->dlam = 1.0 / (double)h->L;                           // ledh.py:133
   double lam = 0.0;
   for (int j = 0; j < h->L; ++j) {                        // ledh.py:134-137
@@ -490,7 +489,7 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
   h->ratio = o->resample_ess_ratio;
   h->seed = o->seed;
   h->device = o->device;
-  h->shared = ops->flow_shared && o->flow_mode == PF_LEDH_FLOW_AUTO;
+  h->shared = ops->flow_shared && o->flow_mode == PF_LEDH_FLOW_AUTO && (algo != 0 || table_fits);
   h->q_diag = is_diag(Qi.data(), nx);
   h->r_diag = is_diag(Ri.data(), nz);
   h->G = (int)((h->N + LT - 1) / LT);

@@ -759,37 +759,31 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 #ifndef PF_PUBW
 #define PF_PUBW (RNW - 1)
 #endif
-      // combine the wave partials; lanes 0..6 publish.  The last wave does it: waves
-      // 0..RCW-1 carry the verification summaries, so the work is spread over waves.
-      if (w == PF_PUBW) {
-        const int j = lane & (RNW - 1);
-        const bool inr = lane < RNW;
-        const double* ms = mslot[cur][j];
-        const double v0 = ms[0], v1 = ms[1], v2 = ms[2], v3 = ms[3], v4 = ms[4], v5 = ms[5], v6 = ms[6];
-        const float mj = inr ? (float)v0 : -INFINITY;
-        const float Mt = row_max_f(mj);
-        const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
-        const double t0 = row_sum_d(inr ? v1 * (double)fj : 0.0);
-        const float t00 = row_sum_f(inr ? (float)v2 * fj * fj : 0.0f);
-        const float t1 = row_sum_f(inr ? (float)v3 * fj : 0.0f);
-        const float t2 = row_sum_f(inr ? (float)v4 * fj : 0.0f);
-        const double ta1 = rec_aux ? row_sum_d(inr ? v5 : 0.0) : 0.0;
-        const double ta2 = rec_aux ? row_sum_d(inr ? v6 : 0.0) : 0.0;
-        if (lane < RF * RCOPIES) {  // RF granules x RCOPIES replicas, one sc1 store (the data is its own flag)
-          // the row reductions above left the record in row 0 (lanes 0..15): lane 0's values
-          // go to every lane, so lanes of all rows store correct replicas
-          const int f = lane % RF, c = lane / RF;
-          const unsigned long long t0b = (unsigned long long)__double_as_longlong(uni(t0));
-          const unsigned pay = f == 0 ? __builtin_amdgcn_readfirstlane(__float_as_uint(Mt))
-                             : f == 1 ? (unsigned)(t0b >> 32)
-                             : f == 2 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t00))
-                             : f == 3 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t1))
-                             : f == 4 ? __builtin_amdgcn_readfirstlane(__float_as_uint(t2))
-                             : f == 5 ? __float_as_uint((float)uni(ta1))
-                             : f == 6 ? __float_as_uint((float)uni(ta2)) : (unsigned)t0b;
-          unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
+      // combine the wave partials and publish.  The last wave does it (waves 0..RCW-1 carry the
+      // verification summaries).  Transposed: lane = granule field + RF * replica, every lane
+      // sums its field over the RNW wave partials itself (a short, independent chain per lane)
+      // instead of a chain of row reductions that the wave would run one after the other.
+      if (w == PF_PUBW && lane < RF * RCOPIES) {
+        const int f = lane % RF, c = lane / RF;
+        const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
+        float Mt = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < RNW; ++j) Mt = fmaxf(Mt, (float)mslot[cur][j][0]);
+        double sum = 0.0;
+        if (src != 0 && (src < 5 || rec_aux)) {
+#pragma unroll
+          for (int j = 0; j < RNW; ++j) {
+            const float mj = (float)mslot[cur][j][0];
+            const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
+            const double v = mslot[cur][j][src];
+            sum += src == 2 ? v * (double)(fj * fj) : (src >= 5 ? v : v * (double)fj);
+          }
         }
+        const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
+        const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
+                           : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
+        unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+        st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
       }
       PF_RCOUNT(14);
       ++s_next;
@@ -799,10 +793,20 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (!verify) continue;
 
     // ---------------- verify step v -------------------------------------------
-    int all = 1;
-#pragma unroll
-    for (int j = 0; j < RCW; ++j) all &= cslot[cur][j][7] != 0.0;
-    all = __builtin_amdgcn_readfirstlane(all);
+    // the RCW (= 4) wave summaries in cslot combine across each quad of lanes (lane & 3 reads
+    // summary lane & 3; quad_perm DPP): independent short chains, the same order everywhere
+    static_assert(RCW == 4, "quad combine of the verification summaries");
+    auto quad_sum = [](double v) {
+      v += dpp_d<DPP_QP_1032>(0.0, v);
+      return v + dpp_d<DPP_QP_2301>(0.0, v);
+    };
+    auto quad_all = [&](int cur_) {
+      int g = cslot[cur_][lane & 3][7] != 0.0;
+      g &= dpp_i<DPP_QP_1032>(0, g);
+      g &= dpp_i<DPP_QP_2301>(0, g);
+      return __builtin_amdgcn_readfirstlane(g);
+    };
+    int all = quad_all(cur);
     PF_RMARK(4);
     for (unsigned spins = 0; !all; ++spins) {  // slow path: not every record was in yet
       PF_RCOUNT(15);
@@ -856,35 +860,28 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         }
       }
       __syncthreads();
-      all = 1;
-#pragma unroll
-      for (int j = 0; j < RCW; ++j) all &= cslot[cur][j][7] != 0.0;
-      all = __builtin_amdgcn_readfirstlane(all);
+      all = quad_all(cur);
     }
     if (!alive) break;
     PF_RMARK(12);  // slow polls
-    double Mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < RCW; ++j) Mx = fmax(Mx, cslot[cur][j][0]);
-    Mx = uni(Mx);
-    double W = 0.0, W2 = 0.0, S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
-#pragma unroll
-    for (int j = 0; j < RCW; ++j) {
-      const double mj = cslot[cur][j][0];
-      const double Fj = (mj > -INFINITY) ? (double)__expf((float)(mj - Mx)) : 0.0;
-      W += cslot[cur][j][1] * Fj;
-      W2 += cslot[cur][j][2] * Fj * Fj;
-      S1 += cslot[cur][j][3] * Fj;
-      S2 += cslot[cur][j][4] * Fj;
-      A1 += cslot[cur][j][5];
-      A2 += cslot[cur][j][6];
+    double Mx, W, W2, S1, S2, A1, A2;
+    {
+      const double* cs = cslot[cur][lane & 3];
+      const double mj = cs[0];
+      double mq = fmax(mj, dpp_d<DPP_QP_1032>(-INFINITY, mj));
+      mq = fmax(mq, dpp_d<DPP_QP_2301>(-INFINITY, mq));
+      const double Fj = (mj > -INFINITY) ? (double)__expf((float)(mj - mq)) : 0.0;
+      const double w1 = quad_sum(cs[1] * Fj), w2 = quad_sum(cs[2] * Fj * Fj);
+      const double s1 = outwg ? quad_sum(cs[3] * Fj) : 0.0, s2 = outwg ? quad_sum(cs[4] * Fj) : 0.0;
+      const double a1 = (outwg && prev_res) ? quad_sum(cs[5]) : 0.0, a2 = (outwg && prev_res) ? quad_sum(cs[6]) : 0.0;
+      Mx = uni(mq);
+      W = uni(w1);
+      W2 = uni(w2);
+      S1 = uni(s1);
+      S2 = uni(s2);
+      A1 = uni(a1);
+      A2 = uni(a2);
     }
-    W = uni(W);
-    W2 = uni(W2);
-    S1 = uni(S1);
-    S2 = uni(S2);
-    A1 = uni(A1);
-    A2 = uni(A2);
     PF_RMARK(4);
     if (!(W > 0.0)) {
       // every particle's weight is zero or NaN (e.g. an all -inf log-likelihood,

@@ -11,9 +11,9 @@ engine's own Philox draws.  Tolerances:
 * fp64 engine (launch-per-step k_step) vs the fp64 oracle: identical decisions, means
   within 1e-9 abs, Neff rel 1e-9;
 * fp32 resident kernel at BASELINE config 2's size (N = 1e6, T = 999) vs the oracle:
-  teacher-forced as in tests/oracle_compare.py (1e-5 / rel 1e-4 up to the first resample,
-  within the Monte-Carlo standard error after it), free-run |dRMSE| <= 1e-4 (the survey
-  measured 4.3e-6 for this wiring);
+  teacher-forced as in tests/oracle_compare.py (1e-5 / rel 1e-4 before the first resample,
+  well inside the filter's own Monte-Carlo error after it), free-run |dRMSE| <= 1e-4 (the
+  survey measured 4.3e-6 for this wiring);
 * fp32 vs fp64 engine, same Philox noise, N = 1e6: |dRMSE| <= 1e-4.
 
 All-dead steps (every weight zero or NaN — e.g. a NaN observation):
