@@ -581,11 +581,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   double aux1 = 0.0, aux2 = 0.0;
   bool last_uniform = false;
   bool alive = true;
-  unsigned long long pg[RF];  // granules of the step being verified (waves 0..RCW-1: one record per lane)
-#pragma unroll
-  for (int f = 0; f < RF; ++f) pg[f] = 0;
-
   while (alive) {
+    // granules of the step this iteration verifies (waves 0..RCW-1: one record per lane); per
+    // iteration, so they are not carried around the loop (and through the rollback) in VGPRs
+    unsigned long long pg[RF];
+#pragma unroll
+    for (int f = 0; f < RF; ++f) pg[f] = 0;
     const bool computing = tstep < p.T;
     const unsigned s_after = s_next + (computing ? 1u : 0u);
 #if defined(PF_ABLATE) && PF_ABLATE == 1
@@ -766,19 +767,26 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       if (w == PF_PUBW && lane < RF * RCOPIES) {
         const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
-        float Mt = -INFINITY;
+        // all LDS reads first, then branch-free arithmetic (per-lane selects, no divergence)
+        float mjv[RNW];
+        double vv[RNW];
 #pragma unroll
-        for (int j = 0; j < RNW; ++j) Mt = fmaxf(Mt, (float)mslot[cur][j][0]);
-        double sum = 0.0;
-        if (src != 0 && (src < 5 || rec_aux)) {
-#pragma unroll
-          for (int j = 0; j < RNW; ++j) {
-            const float mj = (float)mslot[cur][j][0];
-            const float fj = (mj > -INFINITY) ? __expf(mj - Mt) : 0.0f;
-            const double v = mslot[cur][j][src];
-            sum += src == 2 ? v * (double)(fj * fj) : (src >= 5 ? v : v * (double)fj);
-          }
+        for (int j = 0; j < RNW; ++j) {
+          mjv[j] = (float)mslot[cur][j][0];
+          vv[j] = mslot[cur][j][src];
         }
+        float Mt = mjv[0];
+#pragma unroll
+        for (int j = 1; j < RNW; ++j) Mt = fmaxf(Mt, mjv[j]);
+        const bool sq = src == 2, plain = src >= 5;
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < RNW; ++j) {
+          const float fj = (mjv[j] > -INFINITY) ? __expf(mjv[j] - Mt) : 0.0f;
+          const float wf = sq ? fj * fj : fj;
+          sum = fma(vv[j], plain ? 1.0 : (double)wf, sum);
+        }
+        sum = (src == 0 || (plain && !rec_aux)) ? 0.0 : sum;
         const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
         const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
                            : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
