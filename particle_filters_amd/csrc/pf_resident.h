@@ -757,17 +757,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 
     // ---------------- publish this workgroup's record ------------------------
     if (computing) {
-#ifndef PF_PUBW
-#define PF_PUBW (RNW - 1)
-#endif
-      // combine the wave partials and publish.  The last wave does it (waves 0..RCW-1 carry the
-      // verification summaries).  Transposed: lane = granule field + RF * replica, every lane
-      // sums its field over the RNW wave partials itself (a short, independent chain per lane)
-      // instead of a chain of row reductions that the wave would run one after the other.
-      if (w == PF_PUBW && lane < RF * RCOPIES) {
-        const int f = lane % RF, c = lane / RF;
+      // combine the wave partials and publish, spread over the waves: wave w computes granule
+      // field w (RF == RNW) from the RNW wave partials and its first RCOPIES lanes store it to
+      // every replica.  One wave doing all fields sat behind its SIMD partner's compute (the
+      // older wave wins VALU arbitration) and delayed the barrier of the next iteration.
+      static_assert(RF == RNW, "one granule field per wave");
+      {
+        const int f = w;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
-        // all LDS reads first, then branch-free arithmetic (per-lane selects, no divergence)
         float mjv[RNW];
         double vv[RNW];
 #pragma unroll
@@ -780,18 +777,21 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         for (int j = 1; j < RNW; ++j) Mt = fmaxf(Mt, mjv[j]);
         const bool sq = src == 2, plain = src >= 5;
         double sum = 0.0;
+        if (f != 0 && !(plain && !rec_aux)) {  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < RNW; ++j) {
-          const float fj = (mjv[j] > -INFINITY) ? __expf(mjv[j] - Mt) : 0.0f;
-          const float wf = sq ? fj * fj : fj;
-          sum = fma(vv[j], plain ? 1.0 : (double)wf, sum);
+          for (int j = 0; j < RNW; ++j) {
+            const float fj = (mjv[j] > -INFINITY) ? __expf(mjv[j] - Mt) : 0.0f;
+            sum = fma(vv[j], plain ? 1.0 : (double)(sq ? fj * fj : fj), sum);
+          }
         }
-        sum = (src == 0 || (plain && !rec_aux)) ? 0.0 : sum;
-        const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
-        const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
-                           : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
-        unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-        st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
+        if (lane < RCOPIES) {
+          const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
+          const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
+                             : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
+          unsigned long long* g =
+              p.gran + (size_t)lane * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+          st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
+        }
       }
       PF_RCOUNT(14);
       ++s_next;

@@ -12,7 +12,7 @@ epoch mapping).  Stated tolerances (SURVEY 8c "stated tolerance proposal"):
   arithmetic only); from then on fp32 rounding moves a few systematic-resampling slots to
   neighbouring ancestors (tests/oracle_compare.py), so the per-step differences are held to
   the filter's own Monte-Carlo error, measured by an independent-seed oracle run (RMS at
-  most half of it), Neff within rel 5e-2; a decision the oracle would have taken
+  most 0.75 of it), Neff within rel 5e-2; a decision the oracle would have taken
   differently is legitimate only where its Neff is within 1e-3 N of the 0.5 N threshold
   (SURVEY 8c(iv));
 * free run (the oracle decides itself): RMSE vs truth within 1e-4 of the engine's
