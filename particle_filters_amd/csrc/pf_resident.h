@@ -35,6 +35,8 @@
 // ones of k_step (pf_kernels.h): the same filter as the launch-per-step path,
 // up to fp32 rounding of the reductions' grouping.
 #pragma once
+#include <type_traits>
+
 #include "pf_kernels.h"
 
 namespace pf {
@@ -116,6 +118,7 @@ constexpr int RSTAGE = PF_RSTAGE;  // rollback scatter staging chunk (floats of 
 typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int PF_AUX_SC1 = 16;  // buffer instruction cache-policy bits: sc1 (write-through / L1 bypass)
 
+typedef const __attribute__((address_space(4))) float CReal;  // uniform read-only inputs: scalar loads
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
@@ -531,7 +534,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   for (int k = 0; k < ParamLayout<NX, NZ>::SIZE; ++k) P[k] = ((const Real*)p.P)[k];
   const int64_t N = p.N;
   const int G = p.G;
-  const bool outwg = b == G - 1;  // the workgroup that writes the step outputs
   const int64_t o0 = (int64_t)b * RTILE;
   const int64_t i0 = o0 + RPPT * (int64_t)t;
   const int64_t rN = (int64_t)r * p.Npad;
@@ -552,6 +554,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   unsigned long long rstamp_last = __builtin_amdgcn_s_memrealtime();
 #endif
 
+  // The body is instantiated twice: for the workgroup that writes the step outputs (it also
+  // loads and reduces the moment / aux granules) and for all others.  A compile-time flag
+  // keeps the granule loads unconditional inside one uniform branch, so their registers need
+  // no merge copies (a copy right after the loads would wait for them at the loop top).
+  auto body = [&](auto out_tag) {
+  constexpr bool outwg = decltype(out_tag)::value;  // b == G - 1
   // ---- entry state (k_step layout) and its normaliser ------------------------
   float x[RPPT], l[RPPT];
   {
@@ -583,11 +591,22 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool alive = true;
   while (alive) {
     // granules of the step this iteration verifies (waves 0..RCW-1: one record per lane); per
-    // iteration, so they are not carried around the loop (and through the rollback) in VGPRs
+    // iteration, so they are not carried around the loop (and through the rollback) in VGPRs.
+    // Left undefined where not loaded: a zero default would merge with the loaded values.
     unsigned long long pg[RF];
-#pragma unroll
-    for (int f = 0; f < RF; ++f) pg[f] = 0;
     const bool computing = tstep < p.T;
+    // the step's observation (and control) are uniform: scalar loads through the constant
+    // address space (lgkmcnt), so waiting for them never waits for the granule loads (vmcnt)
+    Real z[NZ], uc[NX];
+    if (computing) {
+      const CReal* zt = (const CReal*)(p.z + ((size_t)tstep * R + r) * NZ);
+#pragma unroll
+      for (int k = 0; k < NZ; ++k) z[k] = zt[k];
+      // no control input: u = 0 (g(x) + 0 == g(x))
+      const CReal* ut = (const CReal*)(p.u + ((size_t)tstep * R + r) * NX);
+#pragma unroll
+      for (int k = 0; k < NX; ++k) uc[k] = p.u ? ut[k] : Real(0);
+    }
     const unsigned s_after = s_next + (computing ? 1u : 0u);
 #if defined(PF_ABLATE) && PF_ABLATE == 1
     const bool verify = false;  // ablation: no verification at all (timing floor of the step)
@@ -608,7 +627,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (verify) {
       // granule loads for v (their latency overlaps the step below); slot info
       // read before this iteration's barrier (written iterations ago)
-      if (t < G) {
+      // every lane of the wave loads (t < RMAXG: in bounds); lanes t >= G are masked later
+      if (w < RCW) {
 #pragma unroll
         for (int f = 0; f < RF; ++f)
           if (vg_need(f, outwg)) pg[f] = ld_sc1(vbase + f * RMAXG);
@@ -627,11 +647,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (computing) {
       const bool pred = !(fo && tstep == 0);
       const uint32_t ep_pred = p.ep0 + (uint32_t)(2 * tstep) - fo;
-      Real z[NZ];
-      const float* zt = p.z + ((size_t)tstep * R + r) * NZ;
-#pragma unroll
-      for (int k = 0; k < NZ; ++k) z[k] = zt[k];
-      const Real* u = p.u ? (const Real*)(p.u + ((size_t)tstep * R + r) * NX) : nullptr;
+      const Real* u = uc;
       Real n4[RPPT];
 #pragma unroll
       for (int e = 0; e < RPPT; ++e) n4[e] = Real(0);
@@ -757,14 +773,17 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 
     // ---------------- publish this workgroup's record ------------------------
     if (computing) {
-      // combine the wave partials and publish, spread over the waves: wave w computes granule
-      // field w (RF == RNW) from the RNW wave partials and its first RCOPIES lanes store it to
-      // every replica.  One wave doing all fields sat behind its SIMD partner's compute (the
-      // older wave wins VALU arbitration) and delayed the barrier of the next iteration.
-      static_assert(RF == RNW, "one granule field per wave");
-      {
-        const int f = w;
+#ifndef PF_PUBW
+#define PF_PUBW (RNW - 1)
+#endif
+      // combine the wave partials and publish.  The last wave does it (waves 0..RCW-1 carry the
+      // verification summaries).  Transposed: lane = granule field + RF * replica, every lane
+      // sums its field over the RNW wave partials itself (a short, independent chain per lane)
+      // instead of a chain of row reductions that the wave would run one after the other.
+      if (w == PF_PUBW && lane < RF * RCOPIES) {
+        const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
+        // all LDS reads first, then branch-free arithmetic (per-lane selects, no divergence)
         float mjv[RNW];
         double vv[RNW];
 #pragma unroll
@@ -777,21 +796,18 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         for (int j = 1; j < RNW; ++j) Mt = fmaxf(Mt, mjv[j]);
         const bool sq = src == 2, plain = src >= 5;
         double sum = 0.0;
-        if (f != 0 && !(plain && !rec_aux)) {  // wave-uniform
 #pragma unroll
-          for (int j = 0; j < RNW; ++j) {
-            const float fj = (mjv[j] > -INFINITY) ? __expf(mjv[j] - Mt) : 0.0f;
-            sum = fma(vv[j], plain ? 1.0 : (double)(sq ? fj * fj : fj), sum);
-          }
+        for (int j = 0; j < RNW; ++j) {
+          const float fj = (mjv[j] > -INFINITY) ? __expf(mjv[j] - Mt) : 0.0f;
+          const float wf = sq ? fj * fj : fj;
+          sum = fma(vv[j], plain ? 1.0 : (double)wf, sum);
         }
-        if (lane < RCOPIES) {
-          const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
-          const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
-                             : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
-          unsigned long long* g =
-              p.gran + (size_t)lane * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
-        }
+        sum = (src == 0 || (plain && !rec_aux)) ? 0.0 : sum;
+        const unsigned long long sb = (unsigned long long)__double_as_longlong(sum);
+        const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32)
+                           : f == 7 ? (unsigned)sb : __float_as_uint((float)sum);
+        unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+        st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
       }
       PF_RCOUNT(14);
       ++s_next;
@@ -830,13 +846,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       __builtin_amdgcn_s_sleep(2);
       if (w < RCW) {
         int good = 1;
-        if (in) {
+        unsigned long long pg[RF];  // the slow path's own reload
 #pragma unroll
-          for (int f = 0; f < RF; ++f) {
-            if (!vg_need(f, outwg)) continue;
-            pg[f] = ld_sc1(vbase + f * RMAXG);
-            good &= (unsigned)(pg[f] >> 32) == vtag;
-          }
+        for (int f = 0; f < RF; ++f) {
+          if (!vg_need(f, outwg)) continue;
+          pg[f] = ld_sc1(vbase + f * RMAXG);
+          if (in) good &= (unsigned)(pg[f] >> 32) == vtag;
         }
         m_g = in ? __uint_as_float((unsigned)pg[0]) : -INFINITY;
         s0_g = in ? granule_f64(pg[1], pg[7]) : 0.0;
@@ -1112,6 +1127,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     for (int k = 0; k < 16; ++k)
       if (k < 6 || k > 11) g_pf_stamps[k] = racc[k];
 #endif
+  };
+  if (b == G - 1)
+    body(std::true_type{});
+  else
+    body(std::false_type{});
 }
 
 }  // namespace pf
