@@ -30,6 +30,8 @@ typedef int32_t pf_status;
 #define PF_E_HIP 4             /* HIP runtime error */
 #define PF_E_UNSUPPORTED 5     /* model shape not compiled into this library */
 #define PF_E_NAN 6             /* every particle weight zero or NaN (all-dead filter) -> FloatingPointError */
+#define PF_E_RETRY 7           /* pf_run_device: the resident grid was not co-resident; nothing computed, state
+                                  unchanged, the handle launches cooperatively from now on: run again */
 
 /* g: transition kinds (pf.py:237 per-particle g(x,u)) */
 #define PF_TRANS_LINEAR 0 /* x' = A x (+ u)                         params: A[nx*nx]         */

@@ -24,6 +24,7 @@ PF_E_NOT_PD = 3
 PF_E_HIP = 4
 PF_E_UNSUPPORTED = 5
 PF_E_NAN = 6
+PF_E_RETRY = 7
 
 PF_TRANS_LINEAR = 0
 PF_TRANS_L96 = 1
@@ -177,6 +178,11 @@ class PFError(RuntimeError):
     pass
 
 
+class PFRetry(PFError):
+    """PF_E_RETRY: a resident launch found its grid not co-resident and computed nothing; the
+    state is unchanged and the next run launches cooperatively."""
+
+
 def check(status: int, what: str = "") -> None:
     """Map a pf_status to the reference's exception types (particle_filter.py)."""
     if status == PF_OK:
@@ -194,6 +200,8 @@ def check(status: int, what: str = "") -> None:
         raise NotImplementedError(msg)
     if status == PF_E_NAN:
         raise FloatingPointError(msg)
+    if status == PF_E_RETRY:
+        raise PFRetry(msg)
     raise PFError(msg)
 
 

@@ -160,6 +160,12 @@ struct pf_handle {
   uint32_t res_tag = 0;           // granule tag base of the next resident launch (ResParams::tag0)
   unsigned long long res_flag = 0; // hand-off flag base of the next resident launch
   bool res_unchecked = false;  // a resident launch whose timeout word is not yet read
+  // plain-launch co-residency check (ResParams::arrive): workgroups counted so far, launch
+  // sequence; after an abort the handle launches cooperatively from then on
+  unsigned long long res_arrive = 0, res_seq = 0;
+  bool res_force_coop = false;
+  // bookkeeping before the last resident run, restored when its launch aborted
+  struct { uint32_t epoch, ep_res; int crec; } res_undo{};
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
   bool last_resident = false;  // the last pf_run_device ran k_resident
   // live kernel timing (pf_set_timing): events recorded on the handle's stream right
@@ -427,6 +433,41 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
 // otherwise *used stays false and the caller runs the launch-per-step loop.
 // PF_RESIDENT=0 disables it (A/B comparisons).
 // ---------------------------------------------------------------------------
+// Process-wide order of resident launches per device: a launch on another stream than the
+// previous one waits (on the device) for that one to finish.
+struct ResOrder {
+  std::mutex mu;
+  hipEvent_t ev[64] = {};
+  hipStream_t last[64] = {};
+};
+ResOrder& res_order() {
+  static ResOrder o;
+  return o;
+}
+void res_serialize_begin(int dev, hipStream_t s) {
+  if (dev < 0 || dev >= 64) return;
+  ResOrder& o = res_order();
+  std::lock_guard<std::mutex> lk(o.mu);
+  if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
+}
+void res_serialize_end(int dev, hipStream_t s) {
+  if (dev < 0 || dev >= 64) return;
+  ResOrder& o = res_order();
+  std::lock_guard<std::mutex> lk(o.mu);
+  if (!o.ev[dev] && hipEventCreateWithFlags(&o.ev[dev], hipEventDisableTiming) != hipSuccess) {
+    o.ev[dev] = nullptr;
+    return;
+  }
+  if (hipEventRecord(o.ev[dev], s) == hipSuccess) o.last[dev] = s;
+}
+// a destroyed stream is no longer "the last one" (the event stays valid)
+void res_serialize_forget(int dev, hipStream_t s) {
+  if (dev < 0 || dev >= 64) return;
+  ResOrder& o = res_order();
+  std::lock_guard<std::mutex> lk(o.mu);
+  if (o.last[dev] == s) o.last[dev] = nullptr;
+}
+
 pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t fo, double* dm,
                        double* dc, double* dn, int32_t* df, double* dl, bool* used) {
   *used = false;
@@ -436,7 +477,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   const int G = (int)((h->N + RTILE - 1) / RTILE);
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
   const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
-  const size_t bytes = (gran_n + 2 * flag_n + 2) * sizeof(unsigned long long);
+  const size_t bytes = (gran_n + 2 * flag_n + 4) * sizeof(unsigned long long);
   // Tags and flag values grow from launch to launch (ResParams::tag0 / flag0), so the
   // sync words are zeroed only when allocated or when the 32-bit tag space would wrap.
   const uint64_t tag_span = 4 * (uint64_t)T + 16;
@@ -458,7 +499,10 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     HIPCHK(hipMemsetAsync(h->rsync, 0, h->rsync_bytes, h->stream));
     h->res_tag = 0;
     h->res_flag = 0;
+    h->res_arrive = 0;
+    h->res_seq = 0;
   }
+  h->res_undo = {h->epoch, h->ep_res, h->crec};
   ResParams q;
   std::memset(&q, 0, sizeof(q));
   q.x_in = (const float*)h->x[h->cx];
@@ -501,10 +545,26 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   // the path - and every replicate's result - does not depend on R or on the sharding).
   const int cap = h->ops->resident_cap ? h->ops->resident_cap() : 0;
   const int Rg = cap >= G ? std::max(1, std::min(h->R, cap / G)) : h->R;
+  // Launch mode: one plain launch that checks its own co-residency (ResParams::arrive; ~17 us
+  // cheaper than a cooperative launch), or cooperative launches when the run needs several
+  // replicate groups (an abort must leave every replicate's state untouched), after an abort
+  // on this handle, or with PF_COOP=1.
+  const char* coop_env = std::getenv("PF_COOP");
+  const bool coop = (coop_env && std::atoi(coop_env) == 1) || h->res_force_coop || Rg < h->R;
+  const size_t arr_off = gran_n + 2 * flag_n + 2;
+  // Resident launches of different handles (streams) on one device never overlap: two grids that
+  // each hold part of the CUs would wait for each other's missing workgroups.
+  res_serialize_begin(h->device, h->stream);
   if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int r0 = 0; r0 < h->R; r0 += Rg) {
     q.r0 = r0;
+    q.arrive = coop ? nullptr : h->rsync + arr_off;
+    q.arrive0 = h->res_arrive;
+    // test hook: one workgroup more than the grid has is awaited, so the check times out and aborts
+    if (const char* ta = std::getenv("PF_TEST_ABORT"); ta && std::atoi(ta) == 1) q.arrive0 += 1;
+    q.seq = ++h->res_seq;
     const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream);
+    if (e == hipSuccess) h->res_arrive += (unsigned long long)G * std::min(Rg, h->R - r0);
     if (e == hipErrorCooperativeLaunchTooLarge && r0 == 0) {
       (void)hipGetLastError();
       return PF_OK;  // not co-resident here: launch-per-step path
@@ -512,6 +572,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
   }
   if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
+  res_serialize_end(h->device, h->stream);
   h->res_tag += (uint32_t)tag_span;
   h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;
@@ -534,10 +595,22 @@ pf_status check_resident(pf_handle* h) {
   unsigned int err = 0;
   HIPCHK(hipMemcpy(&err, (const void*)(h->rsync + gran_n + 2 * flag_n), sizeof(err), hipMemcpyDeviceToHost));
   if (!err) return PF_OK;
-  // The launch wrote its particles and records in place: the state is unusable.  Poison
-  // the handle (the next call reports "not initialized") and clear the word for reuse.
-  h->initialized = false;
   HIPCHK(hipMemset((void*)(h->rsync + gran_n + 2 * flag_n), 0, sizeof(err)));
+  if (err == 16u) {
+    // The plain launch did not get its whole grid resident (other work held CUs) and every
+    // workgroup left before touching any state: undo the run's bookkeeping, launch
+    // cooperatively from now on, and report it (pf_run repeats the run itself).
+    h->epoch = h->res_undo.epoch;
+    h->ep_res = h->res_undo.ep_res;
+    h->crec = h->res_undo.crec;
+    h->res_force_coop = true;
+    h->last_resident = false;
+    return fail(PF_E_RETRY, "k_resident: the grid was not co-resident (other work on the GPU); nothing was "
+                            "computed, the state is unchanged and the next run launches cooperatively");
+  }
+  // The launch wrote its particles and records in place: the state is unusable.  Poison
+  // the handle (the next call reports "not initialized").
+  h->initialized = false;
   if (err & 8u)
     return fail(PF_E_NAN, "every particle weight is zero or NaN (all-dead filter); call initialize() again");
   return fail(PF_E_HIP, "k_resident: inter-workgroup hand-off timed out (code " + std::to_string(err) +
@@ -715,6 +788,7 @@ void pf_destroy(pf_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->stream) res_serialize_forget(h->device, h->stream);
   for (int k = 0; k < 2; ++k) {
     if (h->x[k]) (void)hipFree(h->x[k]);
     if (h->lw[k]) (void)hipFree(h->lw[k]);
@@ -1022,11 +1096,15 @@ pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int3
   st = upload_real(h, dZ, Z, (size_t)T * R * nz);
   if (!st && U) st = upload_real(h, dU, U, (size_t)T * R * nx);
   if (st) return bail(st);
-  st = pf_run_device(h, dZ, dU, T, first_update_only, dm, dc, dn, df, dl);
-  if (st) return bail(st);
-  if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(PF_E_HIP, "pf_run: stream sync failed"));
-  st = check_resident(h);
-  if (st) return bail(st);
+  for (int attempt = 0;; ++attempt) {
+    st = pf_run_device(h, dZ, dU, T, first_update_only, dm, dc, dn, df, dl);
+    if (st) return bail(st);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(PF_E_HIP, "pf_run: stream sync failed"));
+    st = check_resident(h);
+    if (st == PF_E_RETRY && attempt == 0) continue;  // aborted before computing: run again, cooperatively
+    if (st) return bail(st);
+    break;
+  }
   std::vector<int32_t> fl((size_t)T * R);
   std::vector<double> nf((size_t)T * R);
   if ((means && hipMemcpy(means, dm, (size_t)T * R * nx * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||

@@ -156,20 +156,15 @@ void register_mat_models();
 
 template <int NX, int NZ, int TK, int OK>
 struct ResidentLaunch {
-  // Every workgroup of the grid must be co-resident (they hand data to each other
-  // inside the launch), so the kernel is launched cooperatively: the runtime checks
-  // the grid against the device's capacity (hipErrorCooperativeLaunchTooLarge -> the
-  // caller runs the launch-per-step path) and dispatches it so that all workgroups
-  // are resident together.  PF_COOP=0 selects a plain launch after the same check
-  // against the occupancy API (cached per device) — for A/B timing only: a plain
-  // launch cannot guarantee residency when other work shares the GPU.
+  // Every workgroup of the grid must be co-resident (they hand data to each other inside the
+  // launch).  p.arrive == null: cooperative launch (the runtime checks the grid against the
+  // device's capacity and dispatches it so that all workgroups are resident together; it costs
+  // ~17 us per launch).  Otherwise a plain launch after the same check against the occupancy
+  // API, and the kernel verifies co-residency itself before touching any state (res_arrival).
+  // hipErrorCooperativeLaunchTooLarge -> the caller runs the launch-per-step path.
   static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s) {
     const void* fn = (const void*)k_resident<float, NX, NZ, TK, OK>;
-    static const int coop = [] {
-      const char* e = std::getenv("PF_COOP");
-      return (e && std::atoi(e) == 0) ? 0 : 1;
-    }();
-    if (coop) {
+    if (!p.arrive) {
       ResParams q = p;
       void* args[] = {&q};
       return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);

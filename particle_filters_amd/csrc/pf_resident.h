@@ -158,7 +158,13 @@ struct ResParams {
   uint32_t tag0;
   unsigned long long flag0;
   int r0, Rtot;  // first replicate of this launch's group; the handle's replicate count (strides)
+  // Run-time co-residency check of a plain (non-cooperative) launch; null for a cooperative
+  // launch.  arrive[0] counts arrived workgroups over all launches (arrive0 before this one),
+  // arrive[1] holds the decision of the latest launch: (seq << 2) | 1 go, | 2 abort.
+  unsigned long long* arrive;
+  unsigned long long arrive0, seq;
 };
+
 
 // Granules a verifying workgroup reads: every workgroup needs M, S0 (both words), S00
 // (log mass, Neff, decision, rollback prefix); only the output workgroup needs the
@@ -192,6 +198,37 @@ __device__ __forceinline__ void st_sc1_f(float* p, float v) {
 }
 __device__ __forceinline__ float ld_sc1_f(const float* p) {
   return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+constexpr unsigned long long RARRIVE_TICKS = 100000;  // 1 ms of s_memrealtime (100 MHz) for the grid to arrive
+
+// Plain launch: every workgroup must be resident at once (they wait for each other's records).
+// Each workgroup counts itself in, then the first one to see either the whole grid counted or
+// the time limit expired decides for all (compare-and-swap on the decision word): "go" is only
+// decided once every workgroup of the launch is running, so none of them can starve; "abort"
+// makes every workgroup - the late ones too - leave before touching any state (err bit 16: the
+// host reports it with the entry state intact).  Thread 0 only; vector atomics.
+__device__ __forceinline__ bool res_arrival(unsigned long long* arrive, unsigned* err, unsigned long long arrive0,
+                                            unsigned long long seq, unsigned long long total) {
+  atomicAdd(arrive, 1ull);
+  const unsigned long long target = arrive0 + total;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const unsigned long long d = ld_sc1(arrive + 1);
+    if ((d >> 2) == seq) return (d & 3ull) == 1ull;
+    const unsigned long long c = ld_sc1(arrive);
+    const unsigned long long code =
+        c >= target ? 1ull : (__builtin_amdgcn_s_memrealtime() - t0 > RARRIVE_TICKS ? 2ull : 0ull);
+    if (code) {
+      const unsigned long long want = (seq << 2) | code;
+      if (atomicCAS(arrive + 1, d, want) == d) {
+        if (code == 2ull) atomicOr(err, 16u);
+        return code == 1ull;
+      }
+      continue;  // another workgroup decided first: read its decision
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
 }
 
 // A value every lane of the workgroup holds identically: move it to scalar registers.
@@ -510,6 +547,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   // per-wave partials, double-buffered by iteration parity: with ONE barrier per
   // iteration a wave is at most one iteration ahead of any other
   __shared__ double mslot[2][RNW][8];  // this workgroup's step record
+  __shared__ __attribute__((aligned(16))) float mmax[2][RNW];  // the wave maxima again, for one vector read
   __shared__ double cslot[2][RCW][8];  // the verified step's summary (+ tags-complete flag)
   __shared__ int okw[RNW];
   __shared__ double sF[NSNAP];     // frame of each snapshot slot
@@ -543,6 +581,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const unsigned long long* gbase = p.gran + (size_t)(b % RCOPIES) * cstride + (size_t)r * RRING * RF * RMAXG;
   const unsigned long long* gbase0 = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
+  if (p.arrive) {  // plain launch: check co-residency before touching any state
+    __shared__ int go_sh;
+    if (t == 0) go_sh = res_arrival(p.arrive, p.err, p.arrive0, p.seq, (unsigned long long)gridDim.x * gridDim.y) ? 1 : 0;
+    __syncthreads();
+    if (!go_sh) return;
+  }
 #ifdef PF_STAMPS
 #ifndef PF_STAMP_T
 #define PF_STAMP_T 0
@@ -558,7 +602,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   // loads and reduces the moment / aux granules) and for all others.  A compile-time flag
   // keeps the granule loads unconditional inside one uniform branch, so their registers need
   // no merge copies (a copy right after the loads would wait for them at the loop top).
-  auto body = [&](auto out_tag) {
+  auto body = [&, p](auto out_tag) {  // p by value: its fields stay in registers, not kernarg reloads
   constexpr bool outwg = decltype(out_tag)::value;  // b == G - 1
   // ---- entry state (k_step layout) and its normaliser ------------------------
   float x[RPPT], l[RPPT];
@@ -595,18 +639,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     // Left undefined where not loaded: a zero default would merge with the loaded values.
     unsigned long long pg[RF];
     const bool computing = tstep < p.T;
-    // the step's observation (and control) are uniform: scalar loads through the constant
-    // address space (lgkmcnt), so waiting for them never waits for the granule loads (vmcnt)
-    Real z[NZ], uc[NX];
-    if (computing) {
-      const CReal* zt = (const CReal*)(p.z + ((size_t)tstep * R + r) * NZ);
-#pragma unroll
-      for (int k = 0; k < NZ; ++k) z[k] = zt[k];
-      // no control input: u = 0 (g(x) + 0 == g(x))
-      const CReal* ut = (const CReal*)(p.u + ((size_t)tstep * R + r) * NX);
-#pragma unroll
-      for (int k = 0; k < NX; ++k) uc[k] = p.u ? ut[k] : Real(0);
-    }
     const unsigned s_after = s_next + (computing ? 1u : 0u);
 #if defined(PF_ABLATE) && PF_ABLATE == 1
     const bool verify = false;  // ablation: no verification at all (timing floor of the step)
@@ -640,6 +672,19 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         Fv = uni(sF[idx]);
         tv = uni_i64(sT[idx]);
       }
+    }
+    // the step's observation (and control) are uniform: scalar loads through the constant
+    // address space (lgkmcnt), so waiting for them never waits for the granule loads (vmcnt).
+    // Issued after the LDS reads above: an LDS wait with a scalar load in flight is a full wait.
+    Real z[NZ], uc[NX];
+    if (computing) {
+      const CReal* zt = (const CReal*)(p.z + ((size_t)tstep * R + r) * NZ);
+#pragma unroll
+      for (int k = 0; k < NZ; ++k) z[k] = zt[k];
+      // no control input: u = 0 (g(x) + 0 == g(x))
+      const CReal* ut = (const CReal*)(p.u + ((size_t)tstep * R + r) * NX);
+#pragma unroll
+      for (int k = 0; k < NX; ++k) uc[k] = p.u ? ut[k] : Real(0);
     }
     PF_RMARK(0);
 
@@ -704,6 +749,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         a2 = wave_sum_ud(aux2);
       }
       if (lane == 0) {
+        mmax[cur][w] = Mw;
         mslot[cur][w][0] = Mw;
         mslot[cur][w][1] = w0;
         mslot[cur][w][2] = w00;
@@ -784,13 +830,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
         // all LDS reads first, then branch-free arithmetic (per-lane selects, no divergence)
-        float mjv[RNW];
+        static_assert(RNW == 8, "two 16-byte reads of the wave maxima");
+        const float4 ma = *(const float4*)&mmax[cur][0], mb = *(const float4*)&mmax[cur][4];
+        const float mjv[RNW] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
         double vv[RNW];
 #pragma unroll
-        for (int j = 0; j < RNW; ++j) {
-          mjv[j] = (float)mslot[cur][j][0];
-          vv[j] = mslot[cur][j][src];
-        }
+        for (int j = 0; j < RNW; ++j) vv[j] = mslot[cur][j][src];
         float Mt = mjv[0];
 #pragma unroll
         for (int j = 1; j < RNW; ++j) Mt = fmaxf(Mt, mjv[j]);
