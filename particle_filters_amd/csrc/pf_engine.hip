@@ -164,8 +164,14 @@ struct pf_handle {
   // sequence; after an abort the handle launches cooperatively from then on
   unsigned long long res_arrive = 0, res_seq = 0;
   bool res_force_coop = false;
-  // bookkeeping before the last resident run, restored when its launch aborted
-  struct { uint32_t epoch, ep_res; int crec; } res_undo{};
+  // bookkeeping before each resident run not yet checked (check_resident), by launch sequence
+  // number: an aborted launch (and every later one, which aborts too) is undone to its entry
+  struct ResUndo {
+    unsigned long long seq;
+    uint32_t epoch, ep_res;
+    int crec;
+  };
+  std::vector<ResUndo> res_undo;
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
   bool last_resident = false;  // the last pf_run_device ran k_resident
   // live kernel timing (pf_set_timing): events recorded on the handle's stream right
@@ -495,14 +501,17 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     pf_status st = apply_pending(h, nullptr, nullptr, false);
     if (st) return st;
   }
+  const size_t arr_off = gran_n + 2 * flag_n + 2;  // arrival count, first aborted launch
   if (zero) {
     HIPCHK(hipMemsetAsync(h->rsync, 0, h->rsync_bytes, h->stream));
+    HIPCHK(hipMemsetAsync(h->rsync + arr_off + 1, 0xff, sizeof(unsigned long long), h->stream));
     h->res_tag = 0;
     h->res_flag = 0;
     h->res_arrive = 0;
     h->res_seq = 0;
   }
-  h->res_undo = {h->epoch, h->ep_res, h->crec};
+  if (!h->res_unchecked) h->res_undo.clear();
+  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec});
   ResParams q;
   std::memset(&q, 0, sizeof(q));
   q.x_in = (const float*)h->x[h->cx];
@@ -551,19 +560,18 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   // on this handle, or with PF_COOP=1.
   const char* coop_env = std::getenv("PF_COOP");
   const bool coop = (coop_env && std::atoi(coop_env) == 1) || h->res_force_coop || Rg < h->R;
-  const size_t arr_off = gran_n + 2 * flag_n + 2;
+  const char* ta = std::getenv("PF_TEST_ABORT");
+  q.test_abort = (ta && std::atoi(ta) == 1 && !coop) ? 1 : 0;
   // Resident launches of different handles (streams) on one device never overlap: two grids that
   // each hold part of the CUs would wait for each other's missing workgroups.
   res_serialize_begin(h->device, h->stream);
   if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int r0 = 0; r0 < h->R; r0 += Rg) {
     q.r0 = r0;
-    q.arrive = coop ? nullptr : h->rsync + arr_off;
+    q.arrive = h->rsync + arr_off;
     q.arrive0 = h->res_arrive;
-    // test hook: one workgroup more than the grid has is awaited, so the check times out and aborts
-    if (const char* ta = std::getenv("PF_TEST_ABORT"); ta && std::atoi(ta) == 1) q.arrive0 += 1;
     q.seq = ++h->res_seq;
-    const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream);
+    const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream, coop);
     if (e == hipSuccess) h->res_arrive += (unsigned long long)G * std::min(Rg, h->R - r0);
     if (e == hipErrorCooperativeLaunchTooLarge && r0 == 0) {
       (void)hipGetLastError();
@@ -597,12 +605,25 @@ pf_status check_resident(pf_handle* h) {
   if (!err) return PF_OK;
   HIPCHK(hipMemset((void*)(h->rsync + gran_n + 2 * flag_n), 0, sizeof(err)));
   if (err == 16u) {
-    // The plain launch did not get its whole grid resident (other work held CUs) and every
-    // workgroup left before touching any state: undo the run's bookkeeping, launch
-    // cooperatively from now on, and report it (pf_run repeats the run itself).
-    h->epoch = h->res_undo.epoch;
-    h->ep_res = h->res_undo.ep_res;
-    h->crec = h->res_undo.crec;
+    // A plain launch did not get its whole grid resident (other work held CUs): every
+    // workgroup left before touching any state, and so did every launch after it.  Undo the
+    // bookkeeping to that launch's entry, launch cooperatively from now on, and report it
+    // (pf_run repeats the run itself).
+    const size_t arr_off = gran_n + 2 * flag_n + 2;
+    unsigned long long aw[2] = {0, 0};
+    HIPCHK(hipMemcpy(aw, (const void*)(h->rsync + arr_off), sizeof(aw), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset((void*)(h->rsync + arr_off + 1), 0xff, sizeof(unsigned long long)));
+    h->res_arrive = aw[0];
+    const auto u = std::find_if(h->res_undo.begin(), h->res_undo.end(),
+                                [&](const pf_handle::ResUndo& x) { return x.seq == aw[1]; });
+    if (u == h->res_undo.end()) {
+      h->initialized = false;
+      return fail(PF_E_HIP, "k_resident: aborted launch not found; call initialize() again");
+    }
+    h->epoch = u->epoch;
+    h->ep_res = u->ep_res;
+    h->crec = u->crec;
+    h->res_undo.clear();
     h->res_force_coop = true;
     h->last_resident = false;
     return fail(PF_E_RETRY, "k_resident: the grid was not co-resident (other work on the GPU); nothing was "

@@ -33,7 +33,7 @@ struct Ops {
   // register-resident whole-run kernel (scalar fp32 models only; null otherwise).
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
   // cannot be co-resident (the caller then runs the launch-per-step path).
-  hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t);
+  hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t, bool coop);
   int (*resident_cap)();  // workgroups of k_resident co-resident on the current device (0: unknown)
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
@@ -157,14 +157,14 @@ void register_mat_models();
 template <int NX, int NZ, int TK, int OK>
 struct ResidentLaunch {
   // Every workgroup of the grid must be co-resident (they hand data to each other inside the
-  // launch).  p.arrive == null: cooperative launch (the runtime checks the grid against the
-  // device's capacity and dispatches it so that all workgroups are resident together; it costs
-  // ~17 us per launch).  Otherwise a plain launch after the same check against the occupancy
-  // API, and the kernel verifies co-residency itself before touching any state (res_arrival).
+  // launch).  coop: cooperative launch (the runtime checks the grid against the device's
+  // capacity and dispatches it so that all workgroups are resident together; ~10-17 us per
+  // launch).  Otherwise a plain launch after the same check against the occupancy API; the
+  // kernel verifies co-residency itself either way (res_arrive / res_try_abort).
   // hipErrorCooperativeLaunchTooLarge -> the caller runs the launch-per-step path.
-  static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s) {
+  static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s, bool coop) {
     const void* fn = (const void*)k_resident<float, NX, NZ, TK, OK>;
-    if (!p.arrive) {
+    if (coop) {
       ResParams q = p;
       void* args[] = {&q};
       return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);

@@ -158,11 +158,12 @@ struct ResParams {
   uint32_t tag0;
   unsigned long long flag0;
   int r0, Rtot;  // first replicate of this launch's group; the handle's replicate count (strides)
-  // Run-time co-residency check of a plain (non-cooperative) launch; null for a cooperative
-  // launch.  arrive[0] counts arrived workgroups over all launches (arrive0 before this one),
-  // arrive[1] holds the decision of the latest launch: (seq << 2) | 1 go, | 2 abort.
+  // Co-residency check (res_arrive / res_try_abort).  arrive[0]: workgroups arrived over all
+  // launches, plus RABORT per aborted launch (arrive0: its value before this launch); arrive[1]:
+  // the first aborted launch's sequence number (atomicMin; all-ones when none).
   unsigned long long* arrive;
   unsigned long long arrive0, seq;
+  int test_abort;  // test hook: the last workgroup arrives only after the others gave up
 };
 
 
@@ -201,33 +202,31 @@ __device__ __forceinline__ float ld_sc1_f(const float* p) {
 }
 
 constexpr unsigned long long RARRIVE_TICKS = 100000;  // 1 ms of s_memrealtime (100 MHz) for the grid to arrive
+constexpr unsigned long long RABORT = 1ull << 40;      // added to the arrival count by an abort
 
-// Plain launch: every workgroup must be resident at once (they wait for each other's records).
-// Each workgroup counts itself in, then the first one to see either the whole grid counted or
-// the time limit expired decides for all (compare-and-swap on the decision word): "go" is only
-// decided once every workgroup of the launch is running, so none of them can starve; "abort"
-// makes every workgroup - the late ones too - leave before touching any state (err bit 16: the
-// host reports it with the entry state intact).  Thread 0 only; vector atomics.
-__device__ __forceinline__ bool res_arrival(unsigned long long* arrive, unsigned* err, unsigned long long arrive0,
-                                            unsigned long long seq, unsigned long long total) {
-  atomicAdd(arrive, 1ull);
-  const unsigned long long target = arrive0 + total;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+// Co-residency.  The workgroups wait for each other's records, so the whole grid must be
+// resident at once; a plain launch does not promise that (other work may hold CUs), so the
+// kernel checks it.  Each workgroup counts itself in (res_arrive) before it touches any state.
+// Verifying a step needs every workgroup's record, so once any step is verified every
+// workgroup has arrived: nothing else is needed on the normal path.  A workgroup that waits
+// for records for more than 1 ms tries to abort (res_try_abort): a compare-and-swap that adds
+// RABORT to the count, possible only while the count is incomplete - so "abort" and "all
+// arrived" exclude each other.  Workgroups arriving after an abort see it in their count and
+// leave at once; nobody writes state, the host reports PF_E_RETRY.  Thread 0; vector atomics.
+__device__ __forceinline__ unsigned long long res_arrive(unsigned long long* arrive) { return atomicAdd(arrive, 1ull); }
+
+// true: the launch is aborted (leave); false: every workgroup has arrived (keep waiting)
+__device__ __forceinline__ bool res_try_abort(unsigned long long* arrive, unsigned* err, unsigned long long arrive0,
+                                              unsigned long long total, unsigned long long seq) {
   for (;;) {
-    const unsigned long long d = ld_sc1(arrive + 1);
-    if ((d >> 2) == seq) return (d & 3ull) == 1ull;
-    const unsigned long long c = ld_sc1(arrive);
-    const unsigned long long code =
-        c >= target ? 1ull : (__builtin_amdgcn_s_memrealtime() - t0 > RARRIVE_TICKS ? 2ull : 0ull);
-    if (code) {
-      const unsigned long long want = (seq << 2) | code;
-      if (atomicCAS(arrive + 1, d, want) == d) {
-        if (code == 2ull) atomicOr(err, 16u);
-        return code == 1ull;
-      }
-      continue;  // another workgroup decided first: read its decision
+    const unsigned long long w = ld_sc1(arrive), rel = w - arrive0;
+    if (rel >= RABORT) return true;
+    if (rel >= total) return false;
+    if (atomicCAS(arrive, w, w + RABORT) == w) {
+      atomicOr(err, 16u);
+      atomicMin(arrive + 1, seq);
+      return true;
     }
-    __builtin_amdgcn_s_sleep(4);
   }
 }
 
@@ -581,12 +580,17 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const unsigned long long* gbase = p.gran + (size_t)(b % RCOPIES) * cstride + (size_t)r * RRING * RF * RMAXG;
   const unsigned long long* gbase0 = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
-  if (p.arrive) {  // plain launch: check co-residency before touching any state
-    __shared__ int go_sh;
-    if (t == 0) go_sh = res_arrival(p.arrive, p.err, p.arrive0, p.seq, (unsigned long long)gridDim.x * gridDim.y) ? 1 : 0;
+  const unsigned long long total_wg = (unsigned long long)gridDim.x * gridDim.y;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  __shared__ int arr_sh;
+  if (p.test_abort && b == p.G - 1 && blockIdx.y == 0) {  // test hook: arrive after the others gave up
+    if (t == 0)
+      while (ld_sc1(p.arrive) - p.arrive0 < RABORT && __builtin_amdgcn_s_memrealtime() - t_start < 5 * RARRIVE_TICKS)
+        __builtin_amdgcn_s_sleep(8);
     __syncthreads();
-    if (!go_sh) return;
   }
+  unsigned long long arr_old = 0;
+  if (t == 0) arr_old = res_arrive(p.arrive);  // its return is checked after the entry loads
 #ifdef PF_STAMPS
 #ifndef PF_STAMP_T
 #define PF_STAMP_T 0
@@ -618,6 +622,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       l[e] = !v ? -INFINITY : (h0.uniform ? lunif : lr - lse0);
     }
   }
+  if (t == 0) arr_sh = arr_old - p.arrive0 < RABORT;  // arrived after an abort: leave
+  __syncthreads();
+  if (!arr_sh) return;
+#ifdef PF_STAMPS
+  if (b == 0 && r == 0 && t == 0) {  // whole-launch phases: start, loop entry (+ loop exit, end below)
+    g_pf_stamps[16] = t_start;
+    g_pf_stamps[17] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  bool verified_any = false;  // a verified step proves the whole grid has arrived
 
   const int fo = p.first_update_only ? 1 : 0;
   int64_t tstep = 0;       // next filter step to compute
@@ -633,6 +647,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   double aux1 = 0.0, aux2 = 0.0;
   bool last_uniform = false;
   bool alive = true;
+  bool aborted = false;
+  float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
+  int64_t zbase = -64;
   while (alive) {
     // granules of the step this iteration verifies (waves 0..RCW-1: one record per lane); per
     // iteration, so they are not carried around the loop (and through the rollback) in VGPRs.
@@ -648,6 +665,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         vnext < s_after && (s_after - vnext > (unsigned)LAG || tstep + (computing ? 1 : 0) >= p.T);
 #endif
     if (!computing && !verify) break;
+    // observations: a window of 64 steps in one VGPR (lane k: step zbase + k), read per step
+    // with v_readlane; refilled when tstep leaves it (every 64 steps, or after a rollback
+    // across its start) - no memory wait in the step
+    if (NZ == 1 && computing && (tstep < zbase || tstep >= zbase + 64)) {
+      zbase = tstep;
+      const int64_t tl = tstep + lane;
+      zwin = tl < p.T ? p.z[(size_t)tl * R + r] : 0.0f;
+    }
     const int cur = (int)(it & 1u);
     ++it;
     const unsigned v = vnext;
@@ -678,13 +703,20 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     // Issued after the LDS reads above: an LDS wait with a scalar load in flight is a full wait.
     Real z[NZ], uc[NX];
     if (computing) {
-      const CReal* zt = (const CReal*)(p.z + ((size_t)tstep * R + r) * NZ);
+      if constexpr (NZ == 1) {
+        z[0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zwin), (int)(tstep - zbase)));
+      } else {
+        const CReal* zt = (const CReal*)(p.z + ((size_t)tstep * R + r) * NZ);
 #pragma unroll
-      for (int k = 0; k < NZ; ++k) z[k] = zt[k];
-      // no control input: u = 0 (g(x) + 0 == g(x))
-      const CReal* ut = (const CReal*)(p.u + ((size_t)tstep * R + r) * NX);
+        for (int k = 0; k < NZ; ++k) z[k] = zt[k];
+      }
 #pragma unroll
-      for (int k = 0; k < NX; ++k) uc[k] = p.u ? ut[k] : Real(0);
+      for (int k = 0; k < NX; ++k) uc[k] = Real(0);  // no control input: u = 0 (g(x) + 0 == g(x))
+      if (p.u) {
+        const CReal* ut = (const CReal*)(p.u + ((size_t)tstep * R + r) * NX);
+#pragma unroll
+        for (int k = 0; k < NX; ++k) uc[k] = ut[k];
+      }
     }
     PF_RMARK(0);
 
@@ -830,9 +862,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
         // all LDS reads first, then branch-free arithmetic (per-lane selects, no divergence)
-        static_assert(RNW == 8, "two 16-byte reads of the wave maxima");
-        const float4 ma = *(const float4*)&mmax[cur][0], mb = *(const float4*)&mmax[cur][4];
-        const float mjv[RNW] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
+        static_assert(RNW % 4 == 0, "16-byte reads of the wave maxima");
+        float mjv[RNW];
+#pragma unroll
+        for (int j = 0; j < RNW; j += 4) {
+          const float4 m4 = *(const float4*)&mmax[cur][j];
+          mjv[j] = m4.x;
+          mjv[j + 1] = m4.y;
+          mjv[j + 2] = m4.z;
+          mjv[j + 3] = m4.w;
+        }
         double vv[RNW];
 #pragma unroll
         for (int j = 0; j < RNW; ++j) vv[j] = mslot[cur][j][src];
@@ -880,6 +919,17 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     for (unsigned spins = 0; !all; ++spins) {  // slow path: not every record was in yet
       PF_RCOUNT(15);
       __syncthreads();  // every wave has read cslot[cur]
+      if (!verified_any && (spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t_start > RARRIVE_TICKS) {
+        // still no step verified after 1 ms: is the grid resident at all?
+        if (t == 0) arr_sh = res_try_abort(p.arrive, p.err, p.arrive0, total_wg, p.seq) ? 2 : 1;
+        __syncthreads();
+        if (arr_sh == 2) {
+          aborted = true;
+          alive = false;
+          break;
+        }
+        verified_any = true;  // every workgroup has arrived: wait on as usual
+      }
       if (spins >= RSPIN_LIMIT) {
         if (t == 0) {
           err_sh = 1;
@@ -931,6 +981,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       all = quad_all(cur);
     }
     if (!alive) break;
+    verified_any = true;
     PF_RMARK(12);  // slow polls
     double Mx, W, W2, S1, S2, A1, A2;
     {
@@ -1041,6 +1092,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     vnext = s_next;  // the speculative steps after tv are discarded
   }
 
+  if (aborted) return;  // nothing was written: the entry state stays as it was
+#ifdef PF_STAMPS
+  if (b == 0 && r == 0 && t == 0) g_pf_stamps[18] = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- the last step resampled: its post-resample moments -------------------
   if (alive && prev_res) {
     const double a1 = wave_sum_ud(aux1), a2 = wave_sum_ud(aux2);
@@ -1171,6 +1226,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   if (stamp_me)
     for (int k = 0; k < 16; ++k)
       if (k < 6 || k > 11) g_pf_stamps[k] = racc[k];
+  if (b == 0 && r == 0 && t == 0) g_pf_stamps[19] = __builtin_amdgcn_s_memrealtime();
 #endif
   };
   if (b == G - 1)
