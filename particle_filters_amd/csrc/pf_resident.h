@@ -351,6 +351,36 @@ __device__ __forceinline__ int64_t count_below(double x, double U, int64_t N) {
   return c;
 }
 
+// Two exclusive block scans in one pass (one pair of barriers): returns a's exclusive prefix,
+// *tot_a / *tot_b the totals, *excl_b b's exclusive prefix.  red >= 2 * BS / 64 doubles.
+template <int BS>
+__device__ __forceinline__ double block_excl_scan2(double a, double b, double* red, double* tot_a, double* excl_b,
+                                                   double* tot_b) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
+  __syncthreads();
+  if (lane == 63) {
+    red[w] = ia;
+    red[NW + w] = ib;
+  }
+  __syncthreads();
+  double oa = 0.0, ta = 0.0, ob = 0.0, tb = 0.0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    if (i < w) {
+      oa += red[i];
+      ob += red[NW + i];
+    }
+    ta += red[i];
+    tb += red[NW + i];
+  }
+  *tot_a = ta;
+  *tot_b = tb;
+  *excl_b = ob + ib - b;
+  return oa + ia - a;
+}
+
 // Rollback + systematic resampling of one step (pf.py:146-171, 188-218), source-
 // driven: workgroup b owns input tile b (its snapshot in LDS), builds that tile's
 // fp64 CDF segment, and writes each particle into its offspring slots
@@ -400,10 +430,6 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
     wv[e] = (lv[e] > -INFINITY) ? (double)exp_r<float>(lv[e] - mown) : 0.0;
     part += wv[e];
   }
-  double Town;
-  const double off = block_excl_scan<RBS>(part, red, &Town);
-  offs[t] = off;
-  PF_GMARK(6);
   // No hand-off for the tile masses: every workgroup already holds all tiles'
   // verified records {m_g, s0_g} (thread t: tile t), so the global tile prefix is
   // computed from those; each tile then maps its own fp64 CDF exactly onto its
@@ -411,14 +437,17 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // The xn write-after-read hazard across rollbacks is ordered by the granule
   // protocol: a rollback is decided only after every workgroup has published a
   // step computed from its previous gathered read.
-  // ---- global tile prefix in fp64 (fixed order: identical in every workgroup) -
+  // One pair of scans: this tile's exclusive prefix and the global tile prefix (fp64, fixed
+  // order: identical in every workgroup).
   double fg = 0.0, wg = 0.0;
   if (t < G && s0_g > 0.0) {
     fg = exp((double)m_g - Mx);
     wg = s0_g * fg;
   }
-  double Stot;
-  const double run = block_excl_scan<RBS>(wg, red, &Stot);
+  double Town, Stot, run;
+  const double off = block_excl_scan2<RBS>(part, wg, red, &Town, &run, &Stot);
+  offs[t] = off;
+  PF_GMARK(6);
   if (t < G) {
     Pl[t] = run / Stot;
     Ck[t] = fg / Stot;
@@ -451,6 +480,13 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
     }
   }
   const int64_t R0 = count_below(base, U, N), R1 = count_below(hi, U, N);
+  // the hand-off below waits only for the tiles whose offspring land in this workgroup's
+  // output slots [o0, o0 + RTILE) (thread t: tile t; typically this tile and a neighbour)
+  bool is_src = false;
+  if (t < G) {
+    const int64_t c0 = count_below(Pl[t], U, N), c1 = count_below(Pl[t + 1], U, N);
+    is_src = c0 < o0 + (int64_t)RTILE && c1 > o0 && c1 > c0;
+  }
   PF_GMARK(7);
   for (int64_t cs = R0; cs < R1; cs += RSTAGE) {
     const int64_t ce = min(cs + (int64_t)RSTAGE, R1);
@@ -477,14 +513,14 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
     __syncthreads();  // stage is refilled by the next chunk
   }
   PF_GMARK(9);
-  // ---- hand-off 2: the gathered array -----------------------------------------
+  // ---- hand-off: the gathered array (from the source tiles of this workgroup's slots) ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const unsigned long long f2 = flag0 + nres;  // one hand-off per rollback: flags count rollbacks
   if (t == 0) st_sc1(sflag + b, f2);
   for (unsigned spins = 0;; ++spins) {
     int good = 1;
-    if (t < G) good = ld_sc1(sflag + t) >= f2;
+    if (is_src) good = ld_sc1(sflag + t) >= f2;
     if (__syncthreads_and(good)) break;
     if (spins >= RSPIN_LIMIT) {
       if (t == 0) {
@@ -611,16 +647,31 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   // ---- entry state (k_step layout) and its normaliser ------------------------
   float x[RPPT], l[RPPT];
   {
+    // the particles' loads first: their latency overlaps the records' reduction below
+    float lr[RPPT];
+    if (i0 + RPPT <= N) {
+#pragma unroll
+      for (int q4 = 0; q4 < RPV; ++q4) {
+        const float4 xv = *(const float4*)(p.x_in + rN + i0 + 4 * q4), lv = *(const float4*)(p.lw_in + rN + i0 + 4 * q4);
+        x[4 * q4] = xv.x; x[4 * q4 + 1] = xv.y; x[4 * q4 + 2] = xv.z; x[4 * q4 + 3] = xv.w;
+        lr[4 * q4] = lv.x; lr[4 * q4 + 1] = lv.y; lr[4 * q4 + 2] = lv.z; lr[4 * q4 + 3] = lv.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < RPPT; ++e) {
+        const bool v = i0 + e < N;
+        x[e] = v ? p.x_in[rN + i0 + e] : 0.0f;
+        lr[e] = v ? p.lw_in[rN + i0 + e] : -INFINITY;
+      }
+    }
     const Head h0 = prologue<NX, RBS>(p.rec_in + (int64_t)r * RC::SIZE * p.Gk, p.Gk, N, p.thresh, false, false,
                                       false, red, Pl);
     const float lse0 = (float)uni(h0.lse);
+#ifdef PF_STAMPS
+    if (b == 0 && r == 0 && t == 0) g_pf_stamps[20] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
-    for (int e = 0; e < RPPT; ++e) {
-      const bool v = i0 + e < N;
-      x[e] = v ? p.x_in[rN + i0 + e] : 0.0f;
-      const float lr = v ? p.lw_in[rN + i0 + e] : -INFINITY;
-      l[e] = !v ? -INFINITY : (h0.uniform ? lunif : lr - lse0);
-    }
+    for (int e = 0; e < RPPT; ++e) l[e] = (i0 + e >= N) ? -INFINITY : (h0.uniform ? lunif : lr[e] - lse0);
   }
   if (t == 0) arr_sh = arr_old - p.arrive0 < RABORT;  // arrived after an abort: leave
   __syncthreads();
@@ -648,6 +699,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool last_uniform = false;
   bool alive = true;
   bool aborted = false;
+  int last_cur = 0;     // mslot buffer of the last computed step, and its frame
+  double F_last = 0.0;
   float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
   int64_t zbase = -64;
   while (alive) {
@@ -672,6 +725,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       zbase = tstep;
       const int64_t tl = tstep + lane;
       zwin = tl < p.T ? p.z[(size_t)tl * R + r] : 0.0f;
+      // wait for it here, in the rare branch: otherwise the wait lands before every step's
+      // readlane and (vmcnt counts in order) takes the granule loads issued below with it
+      asm volatile("; z window %0" ::"v"(zwin));
     }
     const int cur = (int)(it & 1u);
     ++it;
@@ -804,6 +860,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
       rec_aux = have_aux;
       have_aux = false;
+      last_cur = cur;  // exit records: this step's wave partials and frame
+      F_last = F;
     }
 
     // ---------------- wave-level summary of the step being verified ----------
@@ -1167,58 +1225,54 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   }
 
   // ---- exit state in the k_step layout ---------------------------------------
+  if (i0 + RPPT <= N) {
 #pragma unroll
-  for (int e = 0; e < RPPT; ++e)
-    if (i0 + e < N) {
-      p.x_fin[rN + i0 + e] = x[e];
-      p.lw_fin[rN + i0 + e] = l[e];
+    for (int q4 = 0; q4 < RPV; ++q4) {
+      *(float4*)(p.x_fin + rN + i0 + 4 * q4) = make_float4(x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]);
+      *(float4*)(p.lw_fin + rN + i0 + 4 * q4) = make_float4(l[4 * q4], l[4 * q4 + 1], l[4 * q4 + 2], l[4 * q4 + 3]);
     }
-  // one k_step record per group of KQ threads (k_step tile = 1024 particles)
-  {
-    constexpr int KQ = 1024 / RPPT, KW = KQ / 64;
-    const int q = t / KQ;
-    const int kt = b * (RTILE / 1024) + q;
-    WA acc;
-    acc.init();
+  } else {
 #pragma unroll
     for (int e = 0; e < RPPT; ++e)
       if (i0 + e < N) {
-        Real xe[1] = {x[e]};
-        acc.add(l[e], xe);
+        p.x_fin[rN + i0 + e] = x[e];
+        p.lw_fin[rN + i0 + e] = l[e];
       }
-    const float Mw = wave_max_u(acc.m);
-    const float f = (acc.m > -INFINITY) ? __expf(acc.m - Mw) : 0.0f;
-    double vs[WA::NS];
-#pragma unroll
-    for (int i = 0; i < WA::NS; ++i) vs[i] = wave_sum_ud((double)acc.s[i] * (double)(i == 1 ? f * f : f));
-    __syncthreads();
-    if (lane == 0) {
-      red[w * (WA::NS + 1)] = Mw;
-#pragma unroll
-      for (int i = 0; i < WA::NS; ++i) red[w * (WA::NS + 1) + 1 + i] = vs[i];
-    }
-    __syncthreads();
+  }
+#ifdef PF_STAMPS
+  if (b == 0 && r == 0 && t == 0) g_pf_stamps[21] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // One k_step record per 1024-particle tile (KW waves).  They are the wave partials of the
+  // last computed step (mslot, written before that iteration's barrier), moved to the exit
+  // frame: the live log-weights have only been shifted uniformly since (by F - F_last).
+  {
+    constexpr int KQ = 1024 / RPPT, KW = KQ / 64;
+    static_assert(KW >= 1 && KQ % 64 == 0, "k_step tiles of whole waves");
+    const int q = t / KQ;
+    const int kt = b * (RTILE / 1024) + q;
     if ((t % KQ) == 0 && kt < p.Gk) {
-      double Mq = -INFINITY;
-      for (int j = 0; j < KW; ++j) Mq = fmax(Mq, red[(KW * q + j) * (WA::NS + 1)]);
-      double sum[WA::NS];
-#pragma unroll
-      for (int i = 0; i < WA::NS; ++i) sum[i] = 0.0;
-      for (int j = 0; j < KW; ++j) {
-        const double mj = red[(KW * q + j) * (WA::NS + 1)];
-        const double fj = (mj > -INFINITY) ? (double)__expf((float)(mj - Mq)) : 0.0;
-#pragma unroll
-        for (int i = 0; i < WA::NS; ++i) sum[i] += red[(KW * q + j) * (WA::NS + 1) + 1 + i] * (i == 1 ? fj * fj : fj);
-      }
       double* o = p.rec_fin + (int64_t)r * RC::SIZE * p.Gk;
       for (int f2 = 0; f2 < RC::SIZE; ++f2) o[(int64_t)f2 * p.Gk + kt] = 0.0;
       if (last_uniform) {
         o[(int64_t)RC::UNI * p.Gk + kt] = 1.0;
       } else {
-        o[(int64_t)RC::M * p.Gk + kt] = Mq;
-        o[(int64_t)RC::S0 * p.Gk + kt] = sum[0];
-        o[(int64_t)RC::S00 * p.Gk + kt] = sum[1];
-        for (int i = 0; i < NX + RC::NC; ++i) o[(int64_t)(RC::S1 + i) * p.Gk + kt] = sum[2 + i];
+        const double(*ms)[8] = mslot[last_cur];
+        double Mq = -INFINITY;
+        for (int j = 0; j < KW; ++j) Mq = fmax(Mq, ms[KW * q + j][0]);
+        double s0 = 0.0, s00 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (int j = 0; j < KW; ++j) {
+          const double mj = ms[KW * q + j][0];
+          const double fj = (mj > -INFINITY) ? (double)__expf((float)(mj - Mq)) : 0.0;
+          s0 += ms[KW * q + j][1] * fj;
+          s00 += ms[KW * q + j][2] * fj * fj;
+          s1 += ms[KW * q + j][3] * fj;
+          s2 += ms[KW * q + j][4] * fj;
+        }
+        o[(int64_t)RC::M * p.Gk + kt] = Mq - (F - F_last);
+        o[(int64_t)RC::S0 * p.Gk + kt] = s0;
+        o[(int64_t)RC::S00 * p.Gk + kt] = s00;
+        o[(int64_t)RC::S1 * p.Gk + kt] = s1;
+        if constexpr (RC::COV) o[(int64_t)RC::S2 * p.Gk + kt] = s2;
       }
     }
   }

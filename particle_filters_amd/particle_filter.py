@@ -21,8 +21,12 @@ Differences a user sees:
   ``rng.integers`` draw at construction).  ``rng_mode="host"`` draws exactly the
   reference's stream from ``rng`` (``pf.py:128,160,186,217,236``) and ships it
   to the GPU — the replay mode used to prove parity with the reference.
-* ``precision="fp32"`` (default, particle storage and per-particle arithmetic;
-  reductions and the resampling CDF are always fp64) or ``"fp64"``.
+* ``precision="fp32"`` (default, particle storage and per-particle arithmetic) or
+  ``"fp64"``.  The resampling CDF and the tile masses that place it are fp64 on every
+  path; the launch-per-step kernels combine tiles in fp64, while the whole-run fp32
+  kernel (``k_resident``, scalar state) sums within a 512-particle wave in fp32 and
+  carries the per-tile W2 / moment sums as fp32 (the tile mass S0 as fp64), so its
+  Neff decision and moments are fp32-reduced per tile.
 * ``state`` arrays live on the GPU and are fetched lazily on attribute access.
 """
 

@@ -28,18 +28,19 @@ names = ["loop top (prefetch, decision tail)", "compute", "wave partials + barri
 rb_names = {6: "rb: own tile CDF", 7: "rb: offspring counts", 8: "rb: global prefix", 9: "rb: offspring scatter",
             10: "rb: gathered hand-off", 11: "rb: read+jitter", 12: "slow polls"}
 for rep in range(2):
-    lib.pf_debug_stamps_sv_zero(20)
+    lib.pf_debug_stamps_sv_zero(24)
     NV.check(lib.pf_run_device(pf.handle, C.c_void_p(dZ.data_ptr()), None, T, 0, C.c_void_p(outs[0].data_ptr()),
                                C.c_void_p(outs[1].data_ptr()), C.c_void_p(outs[2].data_ptr()),
                                C.c_void_p(fl.data_ptr()), C.c_void_p(outs[3].data_ptr())))
     NV.check(lib.pf_synchronize(pf.handle))
-    buf = (C.c_ulonglong * 20)()
-    lib.pf_debug_stamps_sv(buf, 20)
+    buf = (C.c_ulonglong * 24)()
+    lib.pf_debug_stamps_sv(buf, 24)
     v = np.array(buf[:], dtype=float)
     steps = max(v[14], 1)
     tot = v[:6].sum()
-    print(f"run {rep}: launch phases (workgroup 0): entry {(v[17] - v[16]) / 100:.2f} us, loop "
-          f"{(v[18] - v[17]) / 100:.2f} us, exit {(v[19] - v[18]) / 100:.2f} us")
+    print(f"run {rep}: launch phases (workgroup 0): entry {(v[17] - v[16]) / 100:.2f} us (prologue "
+          f"{(v[20] - v[16]) / 100:.2f}), loop {(v[18] - v[17]) / 100:.2f} us, exit {(v[19] - v[18]) / 100:.2f} us "
+          f"(state stores {(v[21] - v[18]) / 100:.2f})")
     print(f"run {rep}: steps computed {int(v[14])} rollbacks {int(v[13])} failed polls {int(v[15])} "
           f"total {tot / 100 / T:.2f} us per filter step")
     for k, n in enumerate(names):
