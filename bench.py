@@ -567,7 +567,7 @@ def main():
 
     from particle_filters_amd import _native as NV
     from particle_filters_amd.batch import ParticleFilterBatch
-    from particle_filters_amd.distributed import gather_summaries
+    from particle_filters_amd.distributed import gather_summary_buffers
 
     # the series also covers the CPU baselines' samples (they start at the timed window)
     cpu_need = 0 if (rank != 0 or args.no_cpu_baseline) else wl.cpu_steps * 5
@@ -589,12 +589,31 @@ def main():
     NV.check(lib.pf_set_timing(pf.handle, 1), "pf_set_timing")
 
     def outs(T):
-        f64 = dict(dtype=torch.float64, device=dev)
-        return (torch.zeros((T, Rl, nx), **f64), torch.zeros((T, Rl), **f64),
-                torch.zeros((T, Rl), dtype=torch.int32, device=dev), torch.zeros((T, Rl), **f64))
+        """The run's outputs as views of ONE contiguous float64 buffer (means [T][R][nx], Neff,
+        log normaliser, resample flags as int32), so that the ranks' summaries are gathered by a
+        single collective with no packing kernels in the timed region."""
+        n = T * Rl
+        buf = torch.zeros(n * (nx + 3), dtype=torch.float64, device=dev)
+        means = buf[:n * nx].view(T, Rl, nx)
+        neff = buf[n * nx:n * (nx + 1)].view(T, Rl)
+        lnorm = buf[n * (nx + 1):n * (nx + 2)].view(T, Rl)
+        flags = buf[n * (nx + 2):].view(torch.int32)[:n].view(T, Rl)
+        return means, neff, flags, lnorm, buf
+
+    def unpack(flat, T):
+        """[world * per-rank buffer] -> per-replicate summaries [world*R][T][nx + 3] (after timing)."""
+        n = T * Rl
+        rows = []
+        for b in flat.view(world, -1):
+            m = b[:n * nx].view(T, Rl, nx)
+            ne = b[n * nx:n * (nx + 1)].view(T, Rl, 1)
+            ln = b[n * (nx + 1):n * (nx + 2)].view(T, Rl, 1)
+            fl = b[n * (nx + 2):].view(torch.int32)[:n].view(T, Rl, 1).to(torch.float64)
+            rows.append(torch.cat([m, ne, fl, ln], 2).transpose(0, 1))
+        return torch.cat(rows, 0)
 
     def run(dzz, T, o):
-        means, neff, flags, lnorm = o
+        means, neff, flags, lnorm, _ = o
         st = lib.pf_run_device(pf.handle, NV.C.c_void_p(dzz.data_ptr()), None, T, 0,
                                NV.C.c_void_p(means.data_ptr()), None, NV.C.c_void_p(neff.data_ptr()),
                                NV.C.c_void_p(flags.data_ptr()), NV.C.c_void_p(lnorm.data_ptr()))
@@ -603,28 +622,29 @@ def main():
     engine_stream = torch.cuda.ExternalStream(lib.pf_stream(pf.handle), device=dev)
     done = torch.cuda.Event()
 
-    def job(dzz, T, o):
+    def job(dzz, T, o, gathered):
         """One pass of the timed sequence: T filter steps (outputs written by the kernels in
-        HBM, no host work) and, with several ranks, the RCCL all-gather of the summaries."""
+        HBM, no host work) and, with a process group, ONE RCCL all-gather of every rank's
+        summary buffer (distributed.gather_summary_buffers) - unpacked after the timing."""
         run(dzz, T, o)
         if dist is None:
-            return None
+            return
         done.record(engine_stream)
         torch.cuda.current_stream().wait_event(done)
-        means, neff, flags, lnorm = o
-        summ = torch.cat([means, neff[:, :, None], flags[:, :, None].to(torch.float64), lnorm[:, :, None]], 2)
-        return gather_summaries(summ.transpose(0, 1).contiguous(), Rl * world)
+        gather_summary_buffers(gathered, o[4])
 
     ow, ot = outs(W), outs(K)
-    if W > 0:  # warm-up: the same sequence ahead of the timed window (loads kernels, clocks up the GPU)
-        job(dZw, W, ow)
+    gw = torch.empty(world * ow[4].numel(), dtype=torch.float64, device=dev) if dist else None
+    gt = torch.empty(world * ot[4].numel(), dtype=torch.float64, device=dev) if dist else None
+    if W > 0:  # warm-up: the same sequence ahead of the timed window (loads kernels, sets up RCCL)
+        job(dZw, W, ow, gw)
     torch.cuda.synchronize()
     NV.check(lib.pf_synchronize(pf.handle), "warm-up")
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    gathered = job(dZ, K, ot)
+    job(dZ, K, ot, gt)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -640,8 +660,8 @@ def main():
 
     # posterior quality of every replicate (gathered summaries on several ranks)
     truth = np.asarray(truth_all[W:W + K], float).reshape(K, nx)
-    if gathered is not None:
-        allm = gathered.cpu().numpy()[:, :, :nx]  # [world*R][K][nx]
+    if dist is not None:
+        allm = unpack(gt, K).cpu().numpy()[:, :, :nx]  # [world*R][K][nx]
     else:
         allm = np.transpose(ot[0].cpu().numpy(), (1, 0, 2))
     rmse = [float(np.sqrt(np.mean((allm[r] - truth) ** 2))) for r in range(allm.shape[0])]

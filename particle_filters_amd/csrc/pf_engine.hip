@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/pf_engine.h"
+#include "pf_order.h"
 #include "../../include/pf_shard.h"
 #include "pf_diag.h"
 #include "pf_ops.h"
@@ -439,41 +440,6 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
 // otherwise *used stays false and the caller runs the launch-per-step loop.
 // PF_RESIDENT=0 disables it (A/B comparisons).
 // ---------------------------------------------------------------------------
-// Process-wide order of resident launches per device: a launch on another stream than the
-// previous one waits (on the device) for that one to finish.
-struct ResOrder {
-  std::mutex mu;
-  hipEvent_t ev[64] = {};
-  hipStream_t last[64] = {};
-};
-ResOrder& res_order() {
-  static ResOrder o;
-  return o;
-}
-void res_serialize_begin(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64) return;
-  ResOrder& o = res_order();
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
-}
-void res_serialize_end(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64) return;
-  ResOrder& o = res_order();
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (!o.ev[dev] && hipEventCreateWithFlags(&o.ev[dev], hipEventDisableTiming) != hipSuccess) {
-    o.ev[dev] = nullptr;
-    return;
-  }
-  if (hipEventRecord(o.ev[dev], s) == hipSuccess) o.last[dev] = s;
-}
-// a destroyed stream is no longer "the last one" (the event stays valid)
-void res_serialize_forget(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64) return;
-  ResOrder& o = res_order();
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (o.last[dev] == s) o.last[dev] = nullptr;
-}
-
 pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t fo, double* dm,
                        double* dc, double* dn, int32_t* df, double* dl, bool* used) {
   *used = false;
@@ -564,7 +530,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.test_abort = (ta && std::atoi(ta) == 1 && !coop) ? 1 : 0;
   // Resident launches of different handles (streams) on one device never overlap: two grids that
   // each hold part of the CUs would wait for each other's missing workgroups.
-  res_serialize_begin(h->device, h->stream);
+  grid_order_begin(h->device, h->stream);
   if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int r0 = 0; r0 < h->R; r0 += Rg) {
     q.r0 = r0;
@@ -580,7 +546,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
   }
   if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
-  res_serialize_end(h->device, h->stream);
+  grid_order_end(h->device, h->stream);
   h->res_tag += (uint32_t)tag_span;
   h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;
@@ -809,7 +775,7 @@ void pf_destroy(pf_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->stream) res_serialize_forget(h->device, h->stream);
+  if (h->stream) grid_order_forget(h->device, h->stream);
   for (int k = 0; k < 2; ++k) {
     if (h->x[k]) (void)hipFree(h->x[k]);
     if (h->lw[k]) (void)hipFree(h->lw[k]);

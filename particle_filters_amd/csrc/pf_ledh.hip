@@ -18,6 +18,7 @@
 #include "pf_diag.h"
 #include "pf_edh_kernels.h"
 #include "pf_ledh_fused.h"
+#include "pf_order.h"
 
 namespace pf {
 // the engine's thread-local error message (pf_last_error, pf_engine.hip)
@@ -255,6 +256,9 @@ static bool is_diag(const double* A, int n) {
 }  // namespace pf
 
 using namespace pf::ledh;
+using pf::grid_order_begin;
+using pf::grid_order_end;
+using pf::grid_order_forget;
 
 struct pf_ledh_handle {
   const LOps* ops = nullptr;
@@ -580,6 +584,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
     if (p) (void)hipFree(p);
   if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->side) (void)hipStreamDestroy(h->side);
+  if (h->stream) grid_order_forget(h->device, h->stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -871,6 +876,8 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         if (!tables(c0, std::min<int64_t>(65535, T - c0), h->stream))
           st = lfail(PF_E_HIP, "run: batched flow-table launch failed");
     }
+    const bool fused_run = h->fused_nbk > 0 && dTab;
+    if (fused_run) grid_order_begin(h->device, h->stream);  // no overlap with another handle's grid
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
       if (ekf && t % CH == 0 && hipStreamWaitEvent(h->stream, evs[1 + t / CH], 0) != hipSuccess) {
         st = lfail(PF_E_HIP, "run: stream wait failed");
@@ -913,6 +920,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
                         df + t, dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
     }
+    if (fused_run) grid_order_end(h->device, h->stream);
     if (ekf) (void)hipStreamSynchronize(h->side);
     for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     if (st != PF_OK) break;

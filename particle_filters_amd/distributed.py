@@ -81,6 +81,18 @@ def gather_summaries(local, n_replicates: int, group=None):
     return torch.cat(parts, dim=0)
 
 
+def gather_summary_buffers(out, local, group=None):
+    """All-gather equal-sized flat per-rank summary buffers with ONE collective:
+    ``out`` [world * local.numel()] receives rank k's ``local`` at block k (RCCL
+    all_gather_into_tensor; no padding or packing kernels).  For ranks that own equal
+    replicate counts, e.g. bench.py's fixed replicates per rank; ``gather_summaries``
+    handles uneven shards."""
+    import torch.distributed as dist
+
+    dist.all_gather_into_tensor(out, local, group=group)
+    return out
+
+
 def run_sharded(g, h, Q, R, Z, *, mean0, cov0, n_replicates: int, Np: int, group=None,
                 device: int = 0, **pf_kwargs) -> RunResult:
     """Run ``n_replicates`` independent filters sharded over the process group and

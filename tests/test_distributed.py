@@ -103,3 +103,33 @@ def test_gloo_gather_global_replicate_order(world, R):
     for rank, ok, tmax in out:
         assert ok, f"rank {rank}: gathered summaries out of replicate order"
         assert tmax == float(world)
+
+
+def _worker_flat(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = torch.arange(n, dtype=torch.float64) + 1000.0 * rank  # a rank's flat summary buffer
+        out = torch.empty(world * n, dtype=torch.float64)
+        D.gather_summary_buffers(out, local)
+        ref = torch.cat([torch.arange(n, dtype=torch.float64) + 1000.0 * k for k in range(world)])
+        q.put((rank, bool(torch.equal(out, ref))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_flat_summary_buffers_in_rank_order(world):
+    """bench.py's timed-region gather: one all_gather_into_tensor of equal flat buffers."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_flat, args=(r, world, port, 37, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in out:
+        assert ok, f"rank {rank}: flat buffers out of rank order"

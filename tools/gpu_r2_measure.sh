@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-2 measurement pass: full -m gpu suite, smoke, every bench line (the driver's default
+# command first), the spawn launcher, rocprofv3 kernel statistics.  -> gpurun_out/r2meas
+D=gpurun_out/r2meas
+mkdir -p $D
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>; exit status 0/1 go on, anything else ends the pass
+  local name=$1 t=$2
+  shift 2
+  timeout -k 10 $t "$@" > $D/$name.out 2> $D/$name.err
+  local rc=$?
+  echo "$name rc=$rc" | tee -a $D/steps.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 2 ]; then exit $rc; fi
+}
+step tests 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step bench_default 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+step bench_k1000 300 python -u bench.py --steps 1000 --warmup 100 --no-cpu-baseline
+step bench_fp64 300 python -u bench.py --precision fp64 --steps 20 --warmup 5 --no-cpu-baseline
+step bench_spawn 300 python -u bench.py --gpus 1 --spawn --steps 20 --warmup 5 --no-cpu-baseline --no-ref
+step bench_gpus2 120 python -u bench.py --gpus 2 --steps 20 --warmup 5
+step bench_sv64 300 python -u bench.py --workload sv64
+step bench_l96 300 python -u bench.py --workload l96
+step bench_mat 300 python -u bench.py --workload mat
+step bench_ledh 300 python -u bench.py --workload ledh
+step bench_edh 300 python -u bench.py --workload edh
+step bench_ledh_mat 600 python -u bench.py --workload ledh_mat
+step prof_default 300 rocprofv3 --kernel-trace --stats -d $D/prof_default -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-ref
+step prof_k1000 300 rocprofv3 --kernel-trace --stats -d $D/prof_k1000 -o run -- python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-ref
+step prof_sv64 300 rocprofv3 --kernel-trace --stats -d $D/prof_sv64 -o run -- python3 bench.py --workload sv64 --no-cpu-baseline --no-ref
+step prof_l96 300 rocprofv3 --kernel-trace --stats -d $D/prof_l96 -o run -- python3 bench.py --workload l96 --no-cpu-baseline --no-ref
+step prof_mat 300 rocprofv3 --kernel-trace --stats -d $D/prof_mat -o run -- python3 bench.py --workload mat --no-cpu-baseline --no-ref
+step prof_ledh 300 rocprofv3 --kernel-trace --stats -d $D/prof_ledh -o run -- python3 bench.py --workload ledh --no-cpu-baseline
+echo done >> $D/steps.log
