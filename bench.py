@@ -396,7 +396,9 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
                                    if algo == "ledh" else "whole EDH job: k_ekf_seq + k_edh_setup + per step k_ledh_fused",
                          "flops_per_particle_step": fpp,
                          "flops_note": "the reference formulation's per-particle dense algebra (estimate)"
-                                       if per_particle else "shared-Jacobian flow (see ledh_flops_per_particle)"},
+                                       if per_particle else "shared-Jacobian flow (see ledh_flops_per_particle)",
+                         "valu": pmc_valu("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
+                                          "k_flow_wave" if per_particle else "k_ledh_fused", dev_s * 1e6 / K)},
             "cpu_baseline": cpu,
         }
         if model == "mat" and algo == "ledh":
@@ -675,7 +677,7 @@ def main():
     base_b, res_b = 2 * esz * nx + 2 * esz, 2 * esz * nx + 12.0  # SURVEY.md 8(d) at the storage width
     alg_bytes_run = Np * (K * Rl * base_b + float(local_flags.sum()) * res_b)
     achieved = alg_bytes_run / (device_ms * 1e-3) / 1e9
-    kname = "k_resident" if resident else "k_step"
+    kname = "k_resident" if resident else ("k_step_grp" if nx >= 16 else "k_step")  # large states: group kernel
     traffic, traffic_src = pmc_traffic(wl.name, kname)
     G, tile, lds = pf.geometry()
     workload_desc, data_desc = wl.describe(world)
