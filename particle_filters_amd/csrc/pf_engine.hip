@@ -165,12 +165,16 @@ struct pf_handle {
   // sequence; after an abort the handle launches cooperatively from then on
   unsigned long long res_arrive = 0, res_seq = 0;
   bool res_force_coop = false;
+  // entry header (ResParams::hdr): id of the last resident run whose exit header still
+  // describes the state (0: none; any other write of the state clears it), run counter
+  unsigned long long res_hdr = 0, res_run = 0;
   // bookkeeping before each resident run not yet checked (check_resident), by launch sequence
   // number: an aborted launch (and every later one, which aborts too) is undone to its entry
   struct ResUndo {
     unsigned long long seq;
     uint32_t epoch, ep_res;
     int crec;
+    unsigned long long hdr;
   };
   std::vector<ResUndo> res_undo;
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
@@ -320,6 +324,7 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
     if (st) return st;
     p.head = h->head;
   }
+  if (writes_x || writes_lw || writes_rec) h->res_hdr = 0;  // the resident exit header no longer applies
   p.x_in = h->x[h->cx];
   p.x_out = h->x[h->cx ^ 1];
   p.lw_in = h->lw[h->clw];
@@ -449,7 +454,8 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   const int G = (int)((h->N + RTILE - 1) / RTILE);
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
   const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
-  const size_t bytes = (gran_n + 2 * flag_n + 4) * sizeof(unsigned long long);
+  const size_t hdr_off = gran_n + 2 * flag_n + 4;  // entry headers [R][4]
+  const size_t bytes = (hdr_off + 4 * (size_t)h->R) * sizeof(unsigned long long);
   // Tags and flag values grow from launch to launch (ResParams::tag0 / flag0), so the
   // sync words are zeroed only when allocated or when the 32-bit tag space would wrap.
   const uint64_t tag_span = 4 * (uint64_t)T + 16;
@@ -475,9 +481,10 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     h->res_flag = 0;
     h->res_arrive = 0;
     h->res_seq = 0;
+    h->res_hdr = 0;
   }
   if (!h->res_unchecked) h->res_undo.clear();
-  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec});
+  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec, h->res_hdr});
   ResParams q;
   std::memset(&q, 0, sizeof(q));
   q.x_in = (const float*)h->x[h->cx];
@@ -515,6 +522,10 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.r_diag = h->r_diag;
   q.rep_base = h->rep_base;
   q.Rtot = h->R;
+  q.hdr = h->rsync + hdr_off;
+  const char* hdr_env = std::getenv("PF_RES_HDR");  // PF_RES_HDR=0: always the records' prologue (tests)
+  q.hdr_in = (hdr_env && std::atoi(hdr_env) == 0) ? 0ull : h->res_hdr;
+  q.hdr_out = ++h->res_run;
   // Replicates are independent filters: when all R do not fit co-resident, groups of as many
   // as fit run one after another (each replicate computes exactly what it computes alone, so
   // the path - and every replicate's result - does not depend on R or on the sharding).
@@ -547,6 +558,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   }
   if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   grid_order_end(h->device, h->stream);
+  h->res_hdr = q.hdr_out;  // the state is now what this run's exit header describes
   h->res_tag += (uint32_t)tag_span;
   h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;
@@ -589,6 +601,7 @@ pf_status check_resident(pf_handle* h) {
     h->epoch = u->epoch;
     h->ep_res = u->ep_res;
     h->crec = u->crec;
+    h->res_hdr = u->hdr;
     h->res_undo.clear();
     h->res_force_coop = true;
     h->last_resident = false;
@@ -832,6 +845,7 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   h->initialized = true;
   h->pending = false;
   h->lcum_valid = false;
+  h->res_hdr = 0;
   return PF_OK;
 }
 
@@ -1296,6 +1310,7 @@ pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, d
   } else if (h->regularize && h->ops->ch > 1 && h->pbase % 4) {
     return fail(PF_E_ARG, "device-RNG jitter of a scalar-state shard needs N_loc % 4 == 0 (or host replay)");
   }
+  h->res_hdr = 0;
   HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, rj,
                              h->seed, (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream));
   h->pending = false;
@@ -1356,6 +1371,7 @@ pf_status pf_set_state(pf_handle* h, const double* particles, const double* weig
         soa[((size_t)r * nx + d) * h->Npad + i] = particles[((size_t)r * h->N + i) * nx + d];
   pf_status st = upload_real(h, h->x[h->cx], soa.data(), soa.size());
   if (st) return st;
+  h->res_hdr = 0;
   h->lcum_valid = false;  // uploaded weights: k_cdf materialises their CDF when a resample needs it
   // records: one tile carrying S0 = 1 at m = 0 (so lse = 0), the rest empty; or uniform
   std::vector<double> rec((size_t)R * h->G * h->ops->rec_size, 0.0);

@@ -164,6 +164,11 @@ struct ResParams {
   unsigned long long* arrive;
   unsigned long long arrive0, seq;
   int test_abort;  // test hook: the last workgroup arrives only after the others gave up
+  // Entry header [R][4] {run id, lse of the exit log-weights (double bits), uniform, -}: written
+  // at exit by workgroup 0 of each replicate (id hdr_out); a launch whose hdr_in matches the
+  // stored id skips the records' prologue (the host invalidates it on any other state write).
+  unsigned long long* hdr;
+  unsigned long long hdr_in, hdr_out;
 };
 
 
@@ -336,19 +341,23 @@ __device__ __forceinline__ double wave_sum_ud(double v) {
 // Number of systematic positions below x: #{ i in [0, N) : (U + i) / N < x },
 // evaluated with the very comparison the reference makes (pf.py:146-171: pos =
 // (U + arange(N)) / N in fp64, ancestor = first j with pos < cdf[j]).
-__device__ __forceinline__ int64_t count_below(double x, double U, int64_t N) {
-  // exactly, (U + i) / N < x  <=>  i < y = x N - U; the fp64 division can only
-  // disagree when (U + i) / N lies within an ulp of x, i.e. when y is within
-  // ~1e-10 of an integer: only then are the candidate positions evaluated the
-  // reference's way.
+__device__ __noinline__ int count_below_exact(double x, double U, int N, int c) {
   const double Nd = (double)N;
-  const double y = fma(x, Nd, -U);
-  const double c0 = ceil(y);
-  if (c0 - y > 1e-7 && y - (c0 - 1.0) > 1e-7) return (int64_t)fmin(fmax(c0, 0.0), Nd);
-  int64_t c = (int64_t)fmin(fmax(c0, 0.0), Nd);
   while (c > 0 && (U + (double)(c - 1)) / Nd >= x) --c;
   while (c < N && (U + (double)c) / Nd < x) ++c;
   return c;
+}
+__device__ __forceinline__ int count_below(double x, double U, int N) {
+  // exactly, (U + i) / N < x  <=>  i < y = x N - U; the fp64 division can only
+  // disagree when (U + i) / N lies within an ulp of x, i.e. when y is within
+  // ~1e-10 of an integer: only then are the candidate positions evaluated the
+  // reference's way (out of line: it is rare).  32-bit slot indices (N < 2^31).
+  const double Nd = (double)N;
+  const double y = fma(x, Nd, -U);
+  const double c0 = ceil(y);
+  const int c = (int)fmin(fmax(c0, 0.0), Nd);
+  if (c0 - y > 1e-7 && y - (c0 - 1.0) > 1e-7) return c;
+  return count_below_exact(x, U, N, c);
 }
 
 // Two exclusive block scans in one pass (one pair of barriers): returns a's exclusive prefix,
@@ -399,8 +408,9 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
                                        uint32_t ep_res, int regularize, const Real* P) {
   using Mo = Model<Real, NX, NZ, TK, OK>;
   const int t = threadIdx.x;
-  const int64_t o0 = (int64_t)b * RTILE;
-  const int64_t i0 = o0 + RPPT * (int64_t)t;
+  const int N32 = (int)N;  // resident grids: N <= RMAXG * RTILE < 2^31
+  const int o0 = b * RTILE;
+  const int i0 = o0 + RPPT * t;
 #ifdef PF_STAMPS
   unsigned long long gstamp_last = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -461,51 +471,51 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   // in chunks and written with coalesced 16-byte sc1 stores.
   const double U = uniform53(seed, 0, rep, ep_res);
   const double base = Pl[b], hi = Pl[b + 1], c = (Town > 0.0) ? (hi - base) / Town : 0.0;
-  const int64_t tile_last = min(o0 + (int64_t)RTILE, N) - 1;
-  int64_t cb[RPPT + 1];  // cb[e] .. cb[e+1]: slots of particle i0 + e (empty past the tile)
+  const int tile_last = min(o0 + RTILE, N32) - 1;
+  int cb[RPPT + 1];  // cb[e] .. cb[e+1]: slots of particle i0 + e (empty past the tile)
   {
     const double xb = (i0 + RPPT - 1 >= tile_last) ? hi : base + c * offs[t + 1];
-    cb[0] = (i0 <= tile_last) ? count_below(base + c * off, U, N) : 0;
+    cb[0] = (i0 <= tile_last) ? count_below(base + c * off, U, N32) : 0;
     double cum = off;
 #pragma unroll
     for (int e = 0; e < RPPT; ++e) {
-      const int64_t j = i0 + e;
+      const int j = i0 + e;
       if (j > tile_last) {
         cb[e + 1] = cb[e];
         continue;
       }
       cum += wv[e];
       const double xe = (e == RPPT - 1 || j == tile_last) ? xb : fmin(base + c * cum, xb);
-      cb[e + 1] = max(count_below(xe, U, N), cb[e]);
+      cb[e + 1] = max(count_below(xe, U, N32), cb[e]);
     }
   }
-  const int64_t R0 = count_below(base, U, N), R1 = count_below(hi, U, N);
+  const int R0 = count_below(base, U, N32), R1 = count_below(hi, U, N32);
   // the hand-off below waits only for the tiles whose offspring land in this workgroup's
   // output slots [o0, o0 + RTILE) (thread t: tile t; typically this tile and a neighbour)
   bool is_src = false;
   if (t < G) {
-    const int64_t c0 = count_below(Pl[t], U, N), c1 = count_below(Pl[t + 1], U, N);
-    is_src = c0 < o0 + (int64_t)RTILE && c1 > o0 && c1 > c0;
+    const int c0 = count_below(Pl[t], U, N32), c1 = count_below(Pl[t + 1], U, N32);
+    is_src = c0 < o0 + RTILE && c1 > o0 && c1 > c0;
   }
   PF_GMARK(7);
-  for (int64_t cs = R0; cs < R1; cs += RSTAGE) {
-    const int64_t ce = min(cs + (int64_t)RSTAGE, R1);
+  for (int cs = R0; cs < R1; cs += RSTAGE) {
+    const int ce = min(cs + RSTAGE, R1);
 #pragma unroll
     for (int e = 0; e < RPPT; ++e) {
-      const int64_t a0 = max(cb[e], cs), a1 = min(cb[e + 1], ce);
-      for (int64_t i = a0; i < a1; ++i) stage[i - cs] = xv[e];
+      const int a0 = max(cb[e], cs), a1 = min(cb[e + 1], ce);
+      for (int i = a0; i < a1; ++i) stage[i - cs] = xv[e];
     }
     __syncthreads();
     // coalesced write of stage[0, ce - cs) to xn[cs, ce): unaligned head/tail scalar
-    const int64_t body0 = (cs + 3) & ~(int64_t)3, body1 = ce & ~(int64_t)3;
+    const int body0 = (cs + 3) & ~3, body1 = ce & ~3;
     if (body0 >= body1) {
-      for (int64_t i = cs + t; i < ce; i += RBS) st_sc1_f(xn + i, stage[i - cs]);
+      for (int i = cs + t; i < ce; i += RBS) st_sc1_f(xn + i, stage[i - cs]);
     } else {
       if (t < body0 - cs) st_sc1_f(xn + cs + t, stage[t]);
       if (t < ce - body1) st_sc1_f(xn + body1 + t, stage[body1 - cs + t]);
       const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(xn, 0, (int)(N * 4), 0x00020000);
-      for (int64_t i = body0 + 4 * (int64_t)t; i < body1; i += 4 * RBS) {
-        const int64_t k = i - cs;
+      for (int i = body0 + 4 * t; i < body1; i += 4 * RBS) {
+        const int k = i - cs;
         const v4f v = {stage[k], stage[k + 1], stage[k + 2], stage[k + 3]};
         __builtin_amdgcn_raw_buffer_store_b128(v, rw, (int)(i * 4), 0, PF_AUX_SC1);
       }
@@ -664,14 +674,32 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         lr[e] = v ? p.lw_in[rN + i0 + e] : -INFINITY;
       }
     }
-    const Head h0 = prologue<NX, RBS>(p.rec_in + (int64_t)r * RC::SIZE * p.Gk, p.Gk, N, p.thresh, false, false,
-                                      false, red, Pl);
-    const float lse0 = (float)uni(h0.lse);
+    // the previous resident run's exit header when it still describes the state (scalar loads:
+    // uniform), else the records' prologue
+    double lse0d = 0.0;
+    bool uniform0 = false;
+    bool have_hdr = false;
+    if (p.hdr_in) {
+      typedef const __attribute__((address_space(4))) unsigned long long cu64;
+      const cu64* hp = (const cu64*)(p.hdr + (size_t)r * 4);
+      if (hp[0] == p.hdr_in) {
+        lse0d = __longlong_as_double((long long)hp[1]);
+        uniform0 = hp[2] != 0ull;
+        have_hdr = true;
+      }
+    }
+    if (!have_hdr) {
+      const Head h0 = prologue<NX, RBS>(p.rec_in + (int64_t)r * RC::SIZE * p.Gk, p.Gk, N, p.thresh, false, false,
+                                        false, red, Pl);
+      lse0d = uni(h0.lse);
+      uniform0 = h0.uniform != 0;
+    }
+    const float lse0 = (float)lse0d;
 #ifdef PF_STAMPS
     if (b == 0 && r == 0 && t == 0) g_pf_stamps[20] = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
-    for (int e = 0; e < RPPT; ++e) l[e] = (i0 + e >= N) ? -INFINITY : (h0.uniform ? lunif : lr[e] - lse0);
+    for (int e = 0; e < RPPT; ++e) l[e] = (i0 + e >= N) ? -INFINITY : (uniform0 ? lunif : lr[e] - lse0);
   }
   if (t == 0) arr_sh = arr_old - p.arrive0 < RABORT;  // arrived after an abort: leave
   __syncthreads();
@@ -699,6 +727,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool last_uniform = false;
   bool alive = true;
   bool aborted = false;
+  double Tlast = 0.0;   // absolute log mass of the last verified (not resampled) step
   int last_cur = 0;     // mslot buffer of the last computed step, and its frame
   double F_last = 0.0;
   float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
@@ -1101,6 +1130,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     prev_res = false;
     if (!dec) {
       Tprev = Tv;
+      Tlast = Tv;
       const float delta = (float)(Tv - F);
 #pragma unroll
       for (int e = 0; e < RPPT; ++e) l[e] = l[e] - delta;  // -inf stays -inf
@@ -1275,6 +1305,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         if constexpr (RC::COV) o[(int64_t)RC::S2 * p.Gk + kt] = s2;
       }
     }
+  }
+  // entry header of the next launch: log sum of the exit log-weights = Tlast - F (the last
+  // verified step's mass in the exit frame: the fp32 residual of the final shift), or uniform
+  if (b == 0 && t == 0 && alive) {
+    unsigned long long* hp = p.hdr + (size_t)r * 4;
+    hp[1] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : Tlast - F);
+    hp[2] = last_uniform ? 1ull : 0ull;
+    hp[0] = p.hdr_out;
   }
 #ifdef PF_STAMPS
   if (stamp_me)

@@ -153,3 +153,24 @@ def test_two_handles_back_to_back(data):
         assert np.array_equal(neff[:, 0], ref.neff[:, 0])
     for pf in pfs:
         pf.close()
+
+
+def test_entry_header_matches_the_records_prologue(data, monkeypatch):
+    """A resident run that follows a resident run takes the previous exit's header (log sum of
+    the exit weights = the last verified mass in the exit frame) instead of reducing the
+    records; PF_RES_HDR=0 forces the prologue.  Both describe the same normaliser up to fp32
+    rounding of the log-weights: same decisions, means within 1e-5, Neff rel 1e-5."""
+    x0, Z = data
+    out = {}
+    for hdr in ("1", "0"):
+        monkeypatch.setenv("PF_RES_HDR", hdr)
+        pf = make()
+        pf.initialize([x0], [[0.5]])
+        pf.run(Z[:23])
+        out[hdr] = pf.run(Z[23:])
+        pf.close()
+    a, b = out["1"], out["0"]
+    assert np.array_equal(a.flags, b.flags)
+    np.testing.assert_allclose(a.means, b.means, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(a.neff, b.neff, rtol=1e-5)
+    np.testing.assert_allclose(a.log_norm, b.log_norm, rtol=0, atol=1e-5)
