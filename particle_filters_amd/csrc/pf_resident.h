@@ -94,17 +94,27 @@ constexpr int RSTAGE = PF_RSTAGE;  // rollback scatter staging chunk (floats of 
   do {                          \
     if (stamp_me) racc[(k)] += 1; \
   } while (0)
-// rare-path phases (rollback): global accumulators, thread 0 of workgroup 0
+// rare-path phases (rollback): register accumulators of thread 0 of workgroup 0, added to the
+// global slots once at the end of the rollback (a global read-modify-write at every mark would
+// put its load latency into the next phase)
 #define PF_GMARK(k)                                                                   \
   do {                                                                                \
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                     \
       const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();               \
-      g_pf_stamps[(k)] += now_ - gstamp_last;                                         \
+      gacc[(k) - 6] += now_ - gstamp_last;                                            \
       gstamp_last = now_;                                                             \
     }                                                                                 \
   } while (0)
+#define PF_GFLUSH()                                                                    \
+  do {                                                                                \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                       \
+      for (int k_ = 0; k_ < 6; ++k_) g_pf_stamps[6 + k_] += gacc[k_];                 \
+  } while (0)
 #else
 #define PF_GMARK(k) \
+  do {              \
+  } while (0)
+#define PF_GFLUSH() \
   do {              \
   } while (0)
 #define PF_RMARK(k) \
@@ -360,6 +370,18 @@ __device__ __forceinline__ int count_below(double x, double U, int N) {
   return count_below_exact(x, U, N, c);
 }
 
+// Inclusive wave scan on the DPP network (row_shr 1/2/4/8 within 16-lane rows, then the row
+// broadcasts): no LDS crossbar round trips.  A fixed order, identical in every workgroup.
+__device__ __forceinline__ double wave_incl_scan_dpp(double v) {
+  v += dpp_d<0x111>(0.0, v);  // row_shr:1
+  v += dpp_d<0x112>(0.0, v);  // row_shr:2
+  v += dpp_d<0x114>(0.0, v);  // row_shr:4
+  v += dpp_d<0x118>(0.0, v);  // row_shr:8
+  v += dpp_d<DPP_ROW_BCAST15, 0xa>(0.0, v);
+  v += dpp_d<DPP_ROW_BCAST31, 0xc>(0.0, v);
+  return v;
+}
+
 // Two exclusive block scans in one pass (one pair of barriers): returns a's exclusive prefix,
 // *tot_a / *tot_b the totals, *excl_b b's exclusive prefix.  red >= 2 * BS / 64 doubles.
 template <int BS>
@@ -367,7 +389,7 @@ __device__ __forceinline__ double block_excl_scan2(double a, double b, double* r
                                                    double* tot_b) {
   constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const double ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
+  const double ia = wave_incl_scan_dpp(a), ib = wave_incl_scan_dpp(b);
   __syncthreads();
   if (lane == 63) {
     red[w] = ia;
@@ -413,6 +435,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   const int i0 = o0 + RPPT * t;
 #ifdef PF_STAMPS
   unsigned long long gstamp_last = __builtin_amdgcn_s_memrealtime();
+  unsigned long long gacc[6] = {0, 0, 0, 0, 0, 0};
 #endif
   float xv[RPPT], lv[RPPT];
 #pragma unroll
@@ -500,10 +523,17 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   PF_GMARK(7);
   for (int cs = R0; cs < R1; cs += RSTAGE) {
     const int ce = min(cs + RSTAGE, R1);
+    // this thread's particles take the contiguous slots [cb[0], cb[RPPT]): one loop over them
+    {
+      int e = 0;
+      const int a1 = min(cb[RPPT], ce);
+      for (int i = max(cb[0], cs); i < a1; ++i) {
+        while (i >= cb[e + 1]) ++e;
+        float xe = xv[0];
 #pragma unroll
-    for (int e = 0; e < RPPT; ++e) {
-      const int a0 = max(cb[e], cs), a1 = min(cb[e + 1], ce);
-      for (int i = a0; i < a1; ++i) stage[i - cs] = xv[e];
+        for (int k = 1; k < RPPT; ++k) xe = (e == k) ? xv[k] : xe;
+        stage[i - cs] = xe;
+      }
     }
     __syncthreads();
     // coalesced write of stage[0, ce - cs) to xn[cs, ce): unaligned head/tail scalar
@@ -537,6 +567,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
         *err_sh = 1;
         atomicOr(err, 2u);
       }
+      PF_GFLUSH();
       return false;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -577,6 +608,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
 #pragma unroll
   for (int q = 0; q < RPV; ++q) sx_slot[q * RBS + t] = make_float4(xo[4 * q], xo[4 * q + 1], xo[4 * q + 2], xo[4 * q + 3]);
   PF_GMARK(11);
+  PF_GFLUSH();
   return true;
 }
 
