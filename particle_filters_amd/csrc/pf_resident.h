@@ -57,6 +57,12 @@ constexpr int RF = 8;              // record granules: M, S0 (high word), S00, S
 #define PF_RLAG 2
 #endif
 constexpr int RLAG = PF_RLAG;      // verification lag (steps)
+#ifndef PF_PUB_PRIO
+#define PF_PUB_PRIO 1
+#endif
+#ifndef PF_PUBW
+#define PF_PUBW (RNW - 1)  // the wave that combines and publishes the workgroup's record
+#endif
 #ifndef PF_RCOPIES
 #define PF_RCOPIES 8
 #endif
@@ -523,17 +529,10 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   PF_GMARK(7);
   for (int cs = R0; cs < R1; cs += RSTAGE) {
     const int ce = min(cs + RSTAGE, R1);
-    // this thread's particles take the contiguous slots [cb[0], cb[RPPT]): one loop over them
-    {
-      int e = 0;
-      const int a1 = min(cb[RPPT], ce);
-      for (int i = max(cb[0], cs); i < a1; ++i) {
-        while (i >= cb[e + 1]) ++e;
-        float xe = xv[0];
 #pragma unroll
-        for (int k = 1; k < RPPT; ++k) xe = (e == k) ? xv[k] : xe;
-        stage[i - cs] = xe;
-      }
+    for (int e = 0; e < RPPT; ++e) {
+      const int a0 = max(cb[e], cs), a1 = min(cb[e + 1], ce);
+      for (int i = a0; i < a1; ++i) stage[i - cs] = xv[e];
     }
     __syncthreads();
     // coalesced write of stage[0, ce - cs) to xn[cs, ce): unaligned head/tail scalar
@@ -886,6 +885,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         }
       }
       PF_RMARK(1);
+#ifdef PF_YOUNG_PRIO
+      if (w >= RCW) __builtin_amdgcn_s_setprio(2);
+#endif
       // wave partials (DPP), one LDS slot per wave
       const float Mw = wave_max_u(m);
       const float fw = (m > -INFINITY) ? __expf(m - Mw) : 0.0f;
@@ -966,17 +968,22 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
     }
     __syncthreads();  // the iteration's one barrier
+#ifdef PF_YOUNG_PRIO
+    if (w >= RCW && w != PF_PUBW) __builtin_amdgcn_s_setprio(0);
+#endif
     PF_RMARK(2);
 
     // ---------------- publish this workgroup's record ------------------------
     if (computing) {
-#ifndef PF_PUBW
-#define PF_PUBW (RNW - 1)
-#endif
       // combine the wave partials and publish.  The last wave does it (waves 0..RCW-1 carry the
       // verification summaries).  Transposed: lane = granule field + RF * replica, every lane
       // sums its field over the RNW wave partials itself (a short, independent chain per lane)
       // instead of a chain of row reductions that the wave would run one after the other.
+#if PF_PUB_PRIO
+      // the publishing wave is the younger of its SIMD's two: without priority it issues only when
+      // the older wave stalls, and the record is on every workgroup's critical path (-4%/step)
+      if (w == PF_PUBW) __builtin_amdgcn_s_setprio(3);
+#endif
       if (w == PF_PUBW && lane < RF * RCOPIES) {
         const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
@@ -1012,6 +1019,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
         st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
       }
+#if PF_PUB_PRIO
+      if (w == PF_PUBW) __builtin_amdgcn_s_setprio(0);
+#endif
       PF_RCOUNT(14);
       ++s_next;
       ++tstep;
