@@ -401,6 +401,7 @@ __device__ void write_outputs(const StepParams& p, const double* rec, const Head
       }
     }
   } else {
+    if (blk >= 2 * NX) return;  // no field of this workgroup (field f is reduced by workgroup f mod nblk)
     double cnt = 0.0;
     if (want_post) {
       for (int k = t; k < G; k += BS) cnt += rec[RC::CNT * G + k];

@@ -1019,7 +1019,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
         st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
       }
-#if PF_PUB_PRIO
+#if PF_PUB_PRIO && !defined(PF_PRIO_STICKY)
       if (w == PF_PUBW) __builtin_amdgcn_s_setprio(0);
 #endif
       PF_RCOUNT(14);
