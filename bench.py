@@ -300,9 +300,9 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
     # the whole job on the device: EKF tracker (k_ekf_seq), all flow tables, then the T flow steps
     res = pf.run(pf.state, Z[W:W + K], tracker="device")
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0  # before the closing barrier (max over ranks below)
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -648,9 +648,12 @@ def main():
     t0 = time.perf_counter()
     job(dZ, K, ot, gt)
     torch.cuda.synchronize()
+    # this rank's clock stops when its device is done; the closing barrier below still brackets
+    # the window, and the max over ranks (all_reduce) gives the job's time without the
+    # barrier's own RCCL round trip
+    elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     NV.check(lib.pf_synchronize(pf.handle), "timed run")  # raises on a hand-off timeout / all-dead filter
     ms = NV.C.c_float()
     NV.check(lib.pf_last_run_ms(pf.handle, NV.C.byref(ms)), "pf_last_run_ms")

@@ -43,6 +43,9 @@ typedef int32_t pf_status;
 #define PF_OBS_SV_EXACT 3 /* exact SV likelihood y_k ~ N(0, beta_k^2 e^{x_k}) (nz==nx) params: beta[nz];
                              log p = -x/2 - y^2 e^{-x}/(2 beta^2): test_dpf_vs_sv_simulator.py:60-97.
                              R is not used (pass any PD matrix, e.g. I). */
+#define PF_OBS_BEARINGS 4 /* angles of a sensor at s: [atan2(x0-s0, x1-s1), atan2(x2-s2, |(x0,x1)-(s0,s1)|)]
+                             (nz==2, nx>=3)                          params: s[3]
+                             (SPF_results_reproduction_example2.ipynb cell 1 e2_measurement_function) */
 
 #define PF_RESAMPLE_SYSTEMATIC 0 /* pf.py:146-171 */
 #define PF_RESAMPLE_MULTINOMIAL 1 /* pf.py:173-186 (any other method string) */
@@ -73,7 +76,12 @@ typedef struct pf_opts {
   int32_t replicate_base;  /* global id of local replicate 0: replicate r draws with counter
                               word replicate_base + r, so sharding replicates over GPUs gives
                               bitwise the same per-replicate results as one GPU */
+  int32_t kernel_path;     /* PF_PATH_*: which step kernels serve the model */
 } pf_opts;
+
+#define PF_PATH_AUTO 0    /* the compiled shape's kernels when (nx, nz, g, h) is in the compiled list,
+                             else the runtime-shape kernels */
+#define PF_PATH_RUNTIME 1 /* always the runtime-shape kernels (pf_dyn.h): any nx, nz */
 
 typedef struct pf_handle pf_handle;
 
@@ -93,8 +101,13 @@ int32_t pf_device_count(void);
  * (+1e-12 I) and Q (+1e-10 I / +1e-12 I fallbacks), allocates device state. */
 pf_status pf_create(const pf_model_desc* model, const pf_opts* opts, pf_handle** out);
 void pf_destroy(pf_handle* h);
-/* Is (nx, nz, trans_kind, obs_kind) compiled into this library? */
+/* Can the engine run (nx, nz, trans_kind, obs_kind)?  Any positive shape whose kinds fit
+ * (EXP_HALF / SV_EXACT: nz == nx; ACOUSTIC: nx % 4 == 0; BEARINGS: nz == 2, nx >= 3). */
 int32_t pf_model_supported(int32_t nx, int32_t nz, int32_t trans_kind, int32_t obs_kind);
+/* Is the shape in the compiled (register-state) list, i.e. does PF_PATH_AUTO pick those kernels? */
+int32_t pf_model_compiled(int32_t nx, int32_t nz, int32_t trans_kind, int32_t obs_kind);
+/* PF_PATH_RUNTIME if the handle runs the runtime-shape kernels, else PF_PATH_AUTO. */
+int32_t pf_kernel_path(pf_handle* h);
 
 /* initialize (pf.py:110-132): particles ~ N(mean_r, cov_r), uniform weights.
  * mean [R][nx], cov [R][nx][nx]; replay_normals [R][N][nx] or NULL (device Philox). */

@@ -167,3 +167,31 @@ def linear(A: np.ndarray, H: np.ndarray, Q: np.ndarray, R: np.ndarray) -> SSM:
 
     return SSM(A.shape[0], H.shape[0], np.asarray(Q, float), np.asarray(R, float),
                g, lambda x: H @ x, g_vec, lambda X: X @ H.T)
+
+
+def bearings_9d(gamma: float = 1e-2, dt: float = 0.1, q: float = 1e-4, r: float = 1e-6) -> SSM:
+    """The 9-D bearings-only SIR of notebooks/SPF_results_reproduction_example2.ipynb:
+    cell 1 ``e2_build_system_matrix`` (A = gamma [[-I, I, 0], [0, -I, I], [0, 0, -I]]),
+    ``e2_measurement_function`` (azimuth atan2(x, y), elevation atan2(z, |(x, y)|), sensor at
+    the origin), ``R = 1e-6 I``; cell 7 ``g_func = x + A x dt``, ``Q = 1e-4 I``."""
+    I3, Z3 = np.eye(3), np.zeros((3, 3))
+    A = gamma * np.vstack((np.hstack((-I3, I3, Z3)), np.hstack((Z3, -I3, I3)), np.hstack((Z3, Z3, -I3))))
+
+    def g(x, u):
+        return x + A @ x * dt
+
+    def h(x):
+        r_xy = np.sqrt(x[0] ** 2 + x[1] ** 2)
+        return np.array([np.arctan2(x[0], x[1]), np.arctan2(x[2], r_xy)])
+
+    def g_vec(X, u):
+        return X + (X @ A.T) * dt
+
+    def h_vec(X):
+        r_xy = np.sqrt(X[:, 0] ** 2 + X[:, 1] ** 2)
+        return np.stack([np.arctan2(X[:, 0], X[:, 1]), np.arctan2(X[:, 2], r_xy)], axis=1)
+
+    ssm = SSM(9, 2, q * np.eye(9), r * np.eye(2), g, h, g_vec, h_vec)
+    ssm.A = A
+    ssm.dt = dt
+    return ssm

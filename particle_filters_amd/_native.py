@@ -32,6 +32,9 @@ PF_OBS_LINEAR = 0
 PF_OBS_EXP_HALF = 1
 PF_OBS_ACOUSTIC = 2
 PF_OBS_SV_EXACT = 3
+PF_OBS_BEARINGS = 4
+PF_PATH_AUTO = 0
+PF_PATH_RUNTIME = 1
 PF_RESAMPLE_SYSTEMATIC = 0
 PF_RESAMPLE_MULTINOMIAL = 1
 PF_PRECISION_FP32 = 0
@@ -58,7 +61,8 @@ class ModelDesc(C.Structure):
 class Opts(C.Structure):
     _fields_ = [("n_particles", C.c_int64), ("n_replicates", C.c_int32), ("resample_method", C.c_int32),
                 ("resample_thresh", C.c_double), ("regularize", C.c_int32), ("precision", C.c_int32),
-                ("seed", C.c_uint64), ("device", C.c_int32), ("replicate_base", C.c_int32)]
+                ("seed", C.c_uint64), ("device", C.c_int32), ("replicate_base", C.c_int32),
+                ("kernel_path", C.c_int32)]
 
 
 class LedhOpts(C.Structure):
@@ -94,6 +98,8 @@ SIGNATURES = {
     "pf_version": (C.c_char_p, []),
     "pf_device_count": (C.c_int32, []),
     "pf_model_supported": (C.c_int32, [C.c_int32] * 4),
+    "pf_model_compiled": (C.c_int32, [C.c_int32] * 4),
+    "pf_kernel_path": (C.c_int32, [_vp]),
     "pf_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(Opts), C.POINTER(_vp)]),
     "pf_destroy": (None, [_vp]),
     "pf_initialize": (C.c_int32, [_vp, _dp, _dp, _dp]),

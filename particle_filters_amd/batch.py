@@ -50,7 +50,7 @@ class ParticleFilterBatch:
     def __init__(self, g, h, Q, R, *, Np: int, n_replicates: int = 1, replicate_base: int = 0,
                  resample_thresh: float = 0.5, resample_method: str = "systematic",
                  regularize_after_resample: bool = False, seed: int = 0, precision: str = "fp32",
-                 device: int = 0):
+                 device: int = 0, kernel_path: str = "auto"):
         if not M.is_device_model(g, h):
             raise NotImplementedError("ParticleFilterBatch needs particle_filters_amd.models g/h")
         self.Q = np.asarray(Q, float)
@@ -65,7 +65,7 @@ class ParticleFilterBatch:
                       N.PF_RESAMPLE_SYSTEMATIC if resample_method == "systematic" else N.PF_RESAMPLE_MULTINOMIAL,
                       float(resample_thresh), int(bool(regularize_after_resample)),
                       N.PF_PRECISION_FP64 if precision == "fp64" else N.PF_PRECISION_FP32,
-                      int(seed), int(device), self.replicate_base)
+                      int(seed), int(device), self.replicate_base, M.kernel_path_code(kernel_path))
         self._h = N.C.c_void_p()
         N.check(N.load().pf_create(N.C.byref(self._desc), N.C.byref(opts), N.C.byref(self._h)), "pf_create")
 

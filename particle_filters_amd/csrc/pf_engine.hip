@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -20,6 +21,7 @@
 #include "pf_order.h"
 #include "../../include/pf_shard.h"
 #include "pf_diag.h"
+#include "pf_dyn_layout.h"
 #include "pf_ops.h"
 #include "pf_resample_w.h"
 
@@ -52,12 +54,49 @@ static void ensure_registered() {
     register_linear_models();
     register_l96_models();
     register_mat_models();
+    register_dyn_models();
   });
 }
+// compiled-shape kernels of exactly (nx, nz, tk, ok, prec), or null
 const Ops* find_ops(int nx, int nz, int tk, int ok, int prec) {
   ensure_registered();
   for (const Ops& o : registry())
+    if (!o.dyn && o.nx == nx && o.nz == nz && o.tk == tk && o.ok == ok && o.prec == prec) return &o;
+  return nullptr;
+}
+// do the kinds fit the shape (pf_model_supported's rules)?
+static bool kinds_fit(int nx, int nz, int tk, int ok) {
+  if (nx <= 0 || nz <= 0) return false;
+  if (tk != PF_TRANS_LINEAR && tk != PF_TRANS_L96) return false;
+  switch (ok) {
+    case PF_OBS_LINEAR: return true;
+    case PF_OBS_EXP_HALF:
+    case PF_OBS_SV_EXACT: return nz == nx;
+    case PF_OBS_ACOUSTIC: return nx % 4 == 0;
+    case PF_OBS_BEARINGS: return nz == 2 && nx >= 3;
+    default: return false;
+  }
+}
+// runtime-shape kernels (pf_dyn.h) for (nx, nz, tk, ok, prec): the registered shape template,
+// materialised once per concrete shape (stable addresses: handles keep the pointer)
+const Ops* find_ops_dyn(int nx, int nz, int tk, int ok, int prec) {
+  ensure_registered();
+  if (!kinds_fit(nx, nz, tk, ok)) return nullptr;
+  static std::mutex mu;
+  static std::deque<Ops> shapes;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Ops& o : shapes)
     if (o.nx == nx && o.nz == nz && o.tk == tk && o.ok == ok && o.prec == prec) return &o;
+  for (const Ops& t : registry())
+    if (t.dyn && t.tk == tk && t.ok == ok && t.prec == prec) {
+      Ops o = t;
+      o.nx = nx;
+      o.nz = nz;
+      o.rec_size = DynRec(nx).SIZE;
+      o.psize = DynLay(nx, nz).SIZE;
+      shapes.push_back(o);
+      return &shapes.back();
+    }
   return nullptr;
 }
 
@@ -133,7 +172,11 @@ struct pf_handle {
   bool chol_q_ok = true;
   int lq_local = 0, lj_local = 0;  // chol(Q) / 0.001 chol(Q) block-diagonal in nx/4 blocks (k_step_grp)
   int sys_cdf = 0;  // systematic ancestors from the materialised CDF (k_cdf) instead of per-tile scans
-  int h_sel = 0;    // LINEAR h is a component selection (StepParams.hcol2k)
+  int h_sel = 0;    // LINEAR h is a component selection (StepParams.hcol2k; runtime-shape kernels: P[EX+2+k])
+  // runtime-shape kernels (pf_dyn.h): per-replicate scratch [R][wrows][Npad], diagonal factors
+  void* wbuf = nullptr;
+  int64_t wrows = 0;
+  int a_diag = 0, lq_diag = 0, lj_diag = 0;
   int32_t hcol2k[64];
   // within-filter sharding (pf_shard.h): global index of particle 0, filter size, CDF epoch
   bool sharded = false;
@@ -226,6 +269,8 @@ bool choose_geometry(pf_handle* h) {
 
 // k_step LDS: base | tile CDF (doubles) + ancestor slots (ints) when gathering | epilogue record staging
 size_t step_lds(const pf_handle* h, bool gather) {
+  if (h->ops->dyn)  // tile CDF / per-particle weights (doubles) + ancestor slots (ints)
+    return base_lds_bytes(h->G) + (size_t)h->tile * (sizeof(double) + sizeof(int));
   const size_t epi = (size_t)h->ops->rec_size * sizeof(double);
   size_t gat = gather ? (size_t)h->tile * (sizeof(double) + sizeof(int)) : 0;
   if (gather && h->sys_cdf) gat += (size_t)SYS_STAGE * h->tile * sizeof(double) + 16;  // staged source tiles
@@ -267,6 +312,13 @@ StepParams base_params(pf_handle* h) {
   p.out_post_step = -1;
   p.z_rs = h->nz;
   p.u_rs = h->nx;
+  p.dnx = h->nx;
+  p.dnz = h->nz;
+  p.wbuf = h->wbuf;
+  p.wrows = h->wrows;
+  p.a_diag = h->a_diag;
+  p.lq_diag = h->lq_diag;
+  p.lj_diag = h->lj_diag;
   return p;
 }
 
@@ -631,8 +683,14 @@ int32_t pf_device_count(void) {
 }
 
 int32_t pf_model_supported(int32_t nx, int32_t nz, int32_t tk, int32_t ok) {
+  return find_ops(nx, nz, tk, ok, PF_PRECISION_FP32) != nullptr || find_ops_dyn(nx, nz, tk, ok, PF_PRECISION_FP32) != nullptr;
+}
+
+int32_t pf_model_compiled(int32_t nx, int32_t nz, int32_t tk, int32_t ok) {
   return find_ops(nx, nz, tk, ok, PF_PRECISION_FP32) != nullptr;
 }
+
+int32_t pf_kernel_path(pf_handle* h) { return (h && h->ops && h->ops->dyn) ? PF_PATH_RUNTIME : PF_PATH_AUTO; }
 
 pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   if (!m || !o || !out) return fail(PF_E_ARG, "null argument");
@@ -642,11 +700,16 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   if (o->n_replicates <= 0) return fail(PF_E_ARG, "n_replicates must be positive");
   if (o->precision != PF_PRECISION_FP32 && o->precision != PF_PRECISION_FP64)
     return fail(PF_E_ARG, "precision must be PF_PRECISION_FP32 or PF_PRECISION_FP64");
-  const Ops* ops = find_ops(m->nx, m->nz, m->trans_kind, m->obs_kind, o->precision);
+  if (o->kernel_path != PF_PATH_AUTO && o->kernel_path != PF_PATH_RUNTIME)
+    return fail(PF_E_ARG, "kernel_path must be PF_PATH_AUTO or PF_PATH_RUNTIME");
+  // the compiled shape's register-state kernels when there are some, else the runtime-shape ones
+  const Ops* ops = o->kernel_path == PF_PATH_RUNTIME ? nullptr
+                                                     : find_ops(m->nx, m->nz, m->trans_kind, m->obs_kind, o->precision);
+  if (!ops) ops = find_ops_dyn(m->nx, m->nz, m->trans_kind, m->obs_kind, o->precision);
   if (!ops)
     return fail(PF_E_UNSUPPORTED, "model (nx=" + std::to_string(m->nx) + ", nz=" + std::to_string(m->nz) +
                                       ", g=" + std::to_string(m->trans_kind) + ", h=" +
-                                      std::to_string(m->obs_kind) + ") is not compiled into libpf_hip");
+                                      std::to_string(m->obs_kind) + ") does not fit its g / h kinds");
   const int nx = m->nx, nz = m->nz;
   // ---- parameters (double, host) -------------------------------------------
   std::vector<double> P((size_t)ops->psize, 0.0);
@@ -671,6 +734,9 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   } else if (m->obs_kind == PF_OBS_ACOUSTIC) {
     if (m->n_obs_params < 2 + 2 * nz || !m->obs_params) return fail(PF_E_ARG, "ACOUSTIC h needs psi, d0, sx[nz], sy[nz]");
     for (int i = 0; i < 2 + 2 * nz; ++i) P[lay_EX + i] = m->obs_params[i];
+  } else if (m->obs_kind == PF_OBS_BEARINGS) {
+    if (m->n_obs_params < 3 || !m->obs_params) return fail(PF_E_ARG, "BEARINGS h needs the sensor position s[3]");
+    for (int i = 0; i < 3; ++i) P[lay_EX + 2 + i] = m->obs_params[i];
   }
   if (!m->Q || !m->R) return fail(PF_E_ARG, "Q and R are required");
   std::vector<double> L;
@@ -740,6 +806,36 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
     if (!h->h_sel)
       for (int c = 0; c < 64; ++c) h->hcol2k[c] = -1;
   }
+  if (ops->dyn) {  // runtime-shape kernels: diagonal factors, selection H, scratch rows
+    auto diag = [&](int off) {
+      for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j)
+          if (i != j && P[off + i * nx + j] != 0.0) return 0;
+      return 1;
+    };
+    h->a_diag = m->trans_kind == PF_TRANS_LINEAR ? diag(lay_A) : 0;
+    h->lq_diag = diag(lay_LQ);
+    h->lj_diag = diag(lay_LJ);
+    h->h_sel = 0;
+    if (m->obs_kind == PF_OBS_LINEAR) {
+      bool sel = true;
+      std::vector<double> cols(nz, 0.0);
+      for (int k = 0; k < nz && sel; ++k) {
+        int ones = 0;
+        for (int c = 0; c < nx; ++c) {
+          const double v = P[lay_H + k * nx + c];
+          if (v == 1.0) { ++ones; cols[k] = c; }
+          else if (v != 0.0) sel = false;
+        }
+        if (ones != 1) sel = false;
+      }
+      if (sel) {
+        for (int k = 0; k < nz; ++k) P[lay_EX + 2 + k] = cols[k];
+        h->h_sel = 1;
+      }
+    }
+    h->wrows = dyn_wrows(m->trans_kind, nx, nz);
+  }
   h->Pd = P;
   if (!choose_geometry(h)) {
     delete h;
@@ -775,6 +871,8 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   if (const char* he = std::getenv("PF_HEAD")) h->head_mode = std::atoi(he) != 0 ? 1 : 0;
   if (hipMalloc((void**)&h->head, (size_t)h->R * HEAD_STRIDE * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of replicate heads failed"));
+  if (h->wrows > 0 && hipMalloc(&h->wbuf, (size_t)h->R * h->wrows * h->Npad * h->esz) != hipSuccess)
+    return cleanup(fail(PF_E_HIP, "hipMalloc of the runtime-shape scratch failed"));
   if (hipMalloc(&h->P, P.size() * h->esz) != hipSuccess || hipMalloc(&h->d_z, (size_t)h->R * nz * h->esz) != hipSuccess ||
       hipMalloc(&h->d_u, (size_t)h->R * nx * h->esz) != hipSuccess ||
       hipMalloc((void**)&h->d_out, out_doubles(h) * sizeof(double)) != hipSuccess)
@@ -800,7 +898,7 @@ void pf_destroy(pf_handle* h) {
   if (h->head) (void)hipFree(h->head);
   for (double* q : h->lcum)
     if (q) (void)hipFree(q);
-  for (void* p : {(void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
+  for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -833,7 +931,7 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   if (!st) {
     const uint32_t ep = h->epoch++;
     hipError_t e = h->ops->init(h->x[h->cx ^ 1], h->rec[h->crec ^ 1], dmean, dL, drep, h->N, h->Npad, h->G, R,
-                                h->seed, ep, h->rep_base, h->pbase, h->stream);
+                                h->seed, ep, h->rep_base, h->pbase, h->stream, nx);
     if (e != hipSuccess) st = fail(PF_E_HIP, std::string("init launch: ") + hipGetErrorString(e));
     h->cx ^= 1;
     h->crec ^= 1;
@@ -1291,7 +1389,8 @@ pf_status pf_shard_offspring(pf_handle* h, double U, double lo, double mass, int
     if (s) return s;
     h->shard_cdf_ep = h->ep_res;
   }
-  HIPCHK(h->ops->shard_offspring(h->x[h->cx], h->N, h->Npad, h->cdf, U, lo, mass, h->n_total, a, n, out, h->stream));
+  HIPCHK(h->ops->shard_offspring(h->x[h->cx], h->N, h->Npad, h->cdf, U, lo, mass, h->n_total, a, n, out, h->stream,
+                                 h->nx));
   HIPCHK(hipStreamSynchronize(h->stream));
   return PF_OK;
 }
@@ -1312,7 +1411,7 @@ pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, d
   }
   h->res_hdr = 0;
   HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, rj,
-                             h->seed, (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream));
+                             h->seed, (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream, h->nx, h->nz));
   h->pending = false;
   h->shard_cdf_ep = 0;
   if (mean || cov) return pf_moments(h, mean, cov);
@@ -1430,7 +1529,7 @@ pf_status pf_moments(pf_handle* h, double* mean, double* cov) {
     return fail(PF_E_HIP, "hipMalloc failed");
   }
   hipError_t e = h->ops->moments(h->x[h->cx], h->lw[h->clw], h->rec[h->crec], h->G, o.lse, h->N, h->Npad, R, dmean,
-                                 dcov, h->stream);
+                                 dcov, h->stream, nx);
   if (e == hipSuccess && mean)
     e = hipMemcpyAsync(mean, dmean, (size_t)R * nx * sizeof(double), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess && cov)

@@ -240,6 +240,12 @@ struct StepParams {
   // ([R][HEAD_STRIDE] doubles); k_step / k_step_grp / k_cdf then read it instead of every
   // workgroup re-reducing all G records (O(R G^2) -> O(R G) record reads).  Null: in-kernel prologue.
   const double* head;
+  // runtime-shape kernels (pf_dyn.h): the model's dimensions, the per-replicate scratch
+  // [R][wrows][Npad] and whether A / chol(Q) / 0.001 chol(Q) are diagonal
+  int dnx, dnz;
+  void* wbuf;
+  int64_t wrows;
+  int a_diag, lq_diag, lj_diag;
 };
 
 struct Head {

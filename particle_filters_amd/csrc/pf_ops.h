@@ -20,15 +20,17 @@ struct Ops {
   int nx, nz, tk, ok, prec;
   int rec_size, ch, tile_max, tile_min, psize;
   int grp;  // the step kernel is k_step_grp (lane groups per particle)
+  int dyn;  // runtime-shape kernels (pf_dyn.h): nx / nz come from StepParams::dnx / dnz and the
+            // trailing nx / nz arguments below; the compiled-shape entries ignore those
   hipError_t (*step)(const StepParams&, dim3, size_t, hipStream_t);
   hipError_t (*finalize)(const StepParams&, int R, hipStream_t);
   hipError_t (*cdf)(const StepParams&, double* cdf_out, dim3, size_t, hipStream_t);
   hipError_t (*head)(const StepParams&, double* head_out, dim3, size_t, hipStream_t);
   hipError_t (*init)(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                      int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, int64_t pbase,
-                     hipStream_t);
+                     hipStream_t, int nx);
   hipError_t (*moments)(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,
-                        int64_t Npad, int R, double* mean, double* cov, hipStream_t);
+                        int64_t Npad, int R, double* mean, double* cov, hipStream_t, int nx);
   void (*prepare)();  // per-device kernel attributes, called once a device is current
   // register-resident whole-run kernel (scalar fp32 models only; null otherwise).
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
@@ -37,10 +39,10 @@ struct Ops {
   int (*resident_cap)();  // workgroups of k_resident co-resident on the current device (0: unknown)
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
-                                double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t);
+                                double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t, int nx);
   hipError_t (*shard_adopt)(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
                             int jitter, const double* rp_jit, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase,
-                            hipStream_t);
+                            hipStream_t, int nx, int nz);
 };
 
 void register_ops(const Ops& o);
@@ -77,7 +79,7 @@ struct Launch {
   }
   static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                          int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch,
-                         int rep_base, int64_t pbase, hipStream_t s) {
+                         int rep_base, int64_t pbase, hipStream_t s, int) {
     const int64_t n = N > G ? N : G;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK), (unsigned)R);
     hipLaunchKernelGGL((k_init<Real, NX>), grid, dim3(BLOCK), 0, s, (Real*)x, rec, (const Real*)mean,
@@ -85,7 +87,7 @@ struct Launch {
     return hipGetLastError();
   }
   static hipError_t moments(const void* x, const void* lw, const double* rec, int G, const double* lse,
-                            int64_t N, int64_t Npad, int R, double* mean, double* cov, hipStream_t s) {
+                            int64_t N, int64_t Npad, int R, double* mean, double* cov, hipStream_t s, int) {
     hipLaunchKernelGGL((k_mom_mean<Real, NX>), dim3(NX, R), dim3(BLOCK), 64 * sizeof(double), s, (const Real*)x,
                        (const Real*)lw, rec, Rec<NX>::SIZE, G, lse, N, Npad, mean);
     if (cov)
@@ -94,7 +96,7 @@ struct Launch {
     return hipGetLastError();
   }
   static hipError_t shard_offspring(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
-                                    double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t s) {
+                                    double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t s, int) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL((k_shard_offspring<Real, NX>), dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
                        (const Real*)x, N, Npad, cdf, U, lo, mass, Ntot, a, n, (Real*)out);
@@ -102,7 +104,7 @@ struct Launch {
   }
   static hipError_t shard_adopt(const void* rows, void* x, int64_t N, int64_t Npad, double* rec, int G, const void* P,
                                 int jitter, const double* rp_jit, uint64_t seed, uint32_t rep, uint32_t ep, int64_t pbase,
-                                hipStream_t s) {
+                                hipStream_t s, int, int) {
     const int64_t n = N > G ? N : G;
     hipLaunchKernelGGL((k_shard_adopt<Real, NX, NZ, TK, OK>), dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
                        s, (const Real*)rows, (Real*)x, N, Npad, rec, G, (const Real*)P, jitter, rp_jit, seed, rep, ep,
@@ -119,6 +121,7 @@ struct Launch {
     o.tile_min = SGrp<NX>::ON ? 256 / SGrp<NX>::GL : BS * StepTraits<Real, NX, NZ, TK, OK>::CH;
     o.psize = ParamLayout<NX, NZ>::SIZE;
     o.grp = SGrp<NX>::ON ? 1 : 0;
+    o.dyn = 0;
     o.step = &step;
     o.finalize = &finalize;
     o.cdf = &cdf;
@@ -153,6 +156,7 @@ void register_sv_models();
 void register_linear_models();
 void register_l96_models();
 void register_mat_models();
+void register_dyn_models();
 
 template <int NX, int NZ, int TK, int OK>
 struct ResidentLaunch {

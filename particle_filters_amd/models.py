@@ -23,6 +23,8 @@ log-squared ``log b^2 + x + E`` (PF_VS notebook cell 6)   ``SVLogSqObservation(b
 MAT joint ``g_joint`` / ``h_joint``                      ``CVTransition(C, dt)`` / ``AcousticObservation(S, psi, d0, C)``
 exact SV ``sv_log_likelihood_fn`` (test_dpf_vs_sv_       ``SVExactObservation(beta)`` (R unused)
 simulator.py:60-97)
+``x + A @ x * dt`` / ``e2_measurement_function``         ``LinearTransition(I + A dt)`` /
+(SPF example 2, 9-D bearings-only SIR)                   ``BearingsObservation(9)``
 ======================================================  =========================================
 """
 
@@ -282,6 +284,31 @@ class SVExactObservation(Observation):
         return float(np.sum(-0.5 * np.log(2 * np.pi) - np.log(sig) - 0.5 * (y / sig) ** 2))
 
 
+class BearingsObservation(Observation):
+    """Azimuth / elevation of the target seen from a sensor at ``s``:
+    ``[atan2(x - sx, y - sy), atan2(z - sz, |(x, y) - (sx, sy)|)]`` with the position in the
+    first three state components (SPF_results_reproduction_example2.ipynb cell 1
+    ``e2_measurement_function``, sensor at the origin; the notebook's 9-D SIR comparison,
+    cell 7).  Runs on the runtime-shape kernels (any nx >= 3)."""
+
+    kind = N.PF_OBS_BEARINGS
+
+    def __init__(self, nx: int = 9, sensor=(0.0, 0.0, 0.0)):
+        self.nx = int(nx)
+        self.nz = 2
+        self.sensor = np.asarray(sensor, float).reshape(3)
+        if self.nx < 3:
+            raise ValueError("bearings need a 3-D position in the state")
+
+    def params(self):
+        return np.ascontiguousarray(self.sensor)
+
+    def __call__(self, x):
+        x = np.asarray(x, float)
+        d = x[:3] - self.sensor
+        return np.array([np.arctan2(d[0], d[1]), np.arctan2(d[2], np.sqrt(d[0] ** 2 + d[1] ** 2))])
+
+
 def observation_noise(h, R):
     """R as the engine takes it: the exact SV likelihood has none (None -> I)."""
     if R is None:
@@ -388,7 +415,22 @@ def describe(g: Transition, h: Observation, Q: np.ndarray, R: np.ndarray):
 
 
 def supported(g: Transition, h: Observation) -> bool:
+    """Can the engine run this pair (any shape whose kinds fit, pf_model_supported)?"""
     return bool(N.load().pf_model_supported(g.nx, h.nz, g.kind, h.kind))
+
+
+def compiled(g: Transition, h: Observation) -> bool:
+    """Is the pair's shape in the compiled register-state list (else the runtime-shape kernels run)?"""
+    return bool(N.load().pf_model_compiled(g.nx, h.nz, g.kind, h.kind))
+
+
+def kernel_path_code(kernel_path: str) -> int:
+    """``"auto"``: the compiled shape's register-state kernels when (nx, nz, g, h) is in the
+    compiled list, else the runtime-shape kernels (any nx, nz, ``csrc/pf_dyn.h``);
+    ``"runtime"``: always the runtime-shape kernels."""
+    if kernel_path not in ("auto", "runtime"):
+        raise ValueError("kernel_path must be 'auto' or 'runtime'")
+    return N.PF_PATH_RUNTIME if kernel_path == "runtime" else N.PF_PATH_AUTO
 
 
 def sv_logsq_observations(Y) -> np.ndarray:

@@ -143,6 +143,7 @@ class ParticleFilter:
         precision: str = "fp32",
         rng_mode: str = "device",
         device: int = 0,
+        kernel_path: str = "auto",
     ) -> None:
         self.g = g
         self.h = h
@@ -164,6 +165,8 @@ class ParticleFilter:
         self.precision = precision
         self.rng_mode = rng_mode
         self.device = int(device)
+        self.kernel_path = kernel_path
+        self._path = M.kernel_path_code(kernel_path)
         if not M.is_device_model(g, h):
             raise NotImplementedError(
                 "the HIP engine runs g/h on the GPU: pass particle_filters_amd.models objects "
@@ -181,10 +184,16 @@ class ParticleFilter:
         lib = N.load()
         opts = N.Opts(n, 1, self._method, self.resample_thresh, int(bool(self.regularize_after_resample)),
                       N.PF_PRECISION_FP64 if self.precision == "fp64" else N.PF_PRECISION_FP32,
-                      seed, self.device, 0)
+                      seed, self.device, 0, self._path)
         h = N.C.c_void_p()
         N.check(lib.pf_create(N.C.byref(self._desc), N.C.byref(opts), N.C.byref(h)), "pf_create")
         return h
+
+    @property
+    def kernel_path_used(self) -> str:
+        """``"runtime"`` when this filter runs the runtime-shape kernels (pf_dyn.h), else
+        ``"compiled"`` (the compiled shape's register-state kernels)."""
+        return "runtime" if N.load().pf_kernel_path(self._handle) == N.PF_PATH_RUNTIME else "compiled"
 
     def __del__(self):
         lib = N._lib
@@ -373,7 +382,7 @@ class ParticleFilter:
     def _create_scratch(self, n: int):
         lib = N.load()
         opts = N.Opts(n, 1, self._method, self.resample_thresh, int(bool(self.regularize_after_resample)),
-                      N.PF_PRECISION_FP64, 0, self.device, 0)
+                      N.PF_PRECISION_FP64, 0, self.device, 0, self._path)
         h = N.C.c_void_p()
         N.check(lib.pf_create(N.C.byref(self._desc), N.C.byref(opts), N.C.byref(h)), "pf_create")
         return h

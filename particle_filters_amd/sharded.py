@@ -105,7 +105,8 @@ def overlap(a: Array, g: int, d: int, n_loc: int):
 class HipShard:
     """One shard = one pf_handle (R = 1) on a device; row buffers are torch device tensors."""
 
-    def __init__(self, desc, keep, nx, n_loc, n_total, rank, thresh, regularize, seed, precision, device):
+    def __init__(self, desc, keep, nx, n_loc, n_total, rank, thresh, regularize, seed, precision, device,
+                 kernel_path="auto"):
         import torch
 
         self._torch = torch
@@ -116,7 +117,8 @@ class HipShard:
         self.dtype = torch.float64 if precision == "fp64" else torch.float32
         lib = N.load()
         opts = N.Opts(n_loc, 1, N.PF_RESAMPLE_SYSTEMATIC, float(thresh), int(bool(regularize)),
-                      N.PF_PRECISION_FP64 if precision == "fp64" else N.PF_PRECISION_FP32, int(seed), int(device), 0)
+                      N.PF_PRECISION_FP64 if precision == "fp64" else N.PF_PRECISION_FP32, int(seed), int(device), 0,
+                      M.kernel_path_code(kernel_path))
         self._h = N.C.c_void_p()
         N.check(lib.pf_create(N.C.byref(desc), N.C.byref(opts), N.C.byref(self._h)), "pf_create")
         N.check(lib.pf_shard_configure(self._h, int(n_total), int(rank)), "pf_shard_configure")
@@ -232,7 +234,7 @@ class ShardedParticleFilter:
     def __init__(self, g, h, Q, R, *, Np: int, resample_thresh: float = 0.5, regularize_after_resample: bool = False,
                  seed: int = 0, precision: str = "fp32", comm: Optional[DistComm] = None, n_shards: int = 1,
                  device: int = 0, devices: Optional[List[int]] = None, shard_factory=None, rng=None,
-                 rng_mode: str = "device"):
+                 rng_mode: str = "device", kernel_path: str = "auto"):
         if not M.is_device_model(g, h):
             raise NotImplementedError("ShardedParticleFilter needs particle_filters_amd.models g / h")
         self.g, self.h = g, h
@@ -261,7 +263,8 @@ class ShardedParticleFilter:
         for j, r in enumerate(self.mine):
             self.shards[r] = make(desc=self._desc, keep=self._keep, nx=self.nx, n_loc=self.n_loc, n_total=self.Np,
                                   rank=r, thresh=self.resample_thresh, regularize=self.regularize_after_resample,
-                                  seed=seed, precision=precision, device=devs[j % len(devs)] if comm is None else device)
+                                  seed=seed, precision=precision, device=devs[j % len(devs)] if comm is None else device,
+                                  kernel_path=kernel_path)
         self.state: Optional[ShardedState] = None
         self._lse_prev = 0.0
         self._neff = float(self.Np)

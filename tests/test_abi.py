@@ -81,7 +81,7 @@ def test_model_registry():
 def _create(g, h, Q, R, **kw):
     d, keep = M.describe(g, h, np.asarray(Q, float), np.asarray(R, float))
     o = dict(n_particles=100, n_replicates=1, resample_method=0, resample_thresh=0.5, regularize=0,
-             precision=0, seed=1, device=0, replicate_base=0)
+             precision=0, seed=1, device=0, replicate_base=0, kernel_path=0)
     o.update(kw)
     opts = NV.Opts(**o)
     h_ = C.c_void_p()
@@ -103,11 +103,49 @@ def test_create_rejects_bad_arguments_before_touching_a_device():
 
 
 def test_create_unsupported_model():
-    A = np.eye(5)
-    st, _ = _create(M.LinearTransition(A), M.LinearObservation(np.ones((1, 5))), np.eye(5), [[1.0]])
-    assert st == NV.PF_E_UNSUPPORTED
+    # kinds that do not fit the shape (EXP_HALF observes every component: nz must equal nx)
+    Q, R, beta = np.eye(5), np.eye(3), np.ones(3)
+    d = NV.ModelDesc(5, 3, NV.PF_TRANS_LINEAR, NV.PF_OBS_EXP_HALF, NV.dptr(np.eye(5).ravel()), 25,
+                     NV.dptr(beta), 3, NV.dptr(Q), NV.dptr(R))
+    opts = NV.Opts(100, 1, 0, 0.5, 0, 0, 1, 0, 0, 0)
+    h_ = C.c_void_p()
+    st = NV.load().pf_create(C.byref(d), C.byref(opts), C.byref(h_))
+    assert st == NV.PF_E_UNSUPPORTED and not h_.value
     with pytest.raises(NotImplementedError):
         NV.check(st)
+
+
+def test_runtime_shape_registry():
+    """Shapes outside the compiled list run on the runtime-shape kernels (pf_dyn.h)."""
+    lib = NV.load()
+    L96, LIN = NV.PF_TRANS_L96, NV.PF_TRANS_LINEAR
+    # the builder's second L96 golden case (nx = 12) and the simulator's default nx = 1000
+    for nx, nz in ((12, 3), (1000, 250), (40, 10)):
+        assert lib.pf_model_supported(nx, nz, L96, NV.PF_OBS_LINEAR)
+    assert lib.pf_model_compiled(40, 10, L96, NV.PF_OBS_LINEAR)
+    assert not lib.pf_model_compiled(12, 3, L96, NV.PF_OBS_LINEAR)
+    # the 9-D bearings-only SIR (SPF example 2)
+    assert lib.pf_model_supported(9, 2, LIN, NV.PF_OBS_BEARINGS)
+    assert not lib.pf_model_supported(9, 3, LIN, NV.PF_OBS_BEARINGS)
+    assert not lib.pf_model_supported(2, 2, LIN, NV.PF_OBS_BEARINGS)
+    assert lib.pf_model_supported(8, 25, LIN, NV.PF_OBS_ACOUSTIC)
+    assert not lib.pf_model_supported(6, 25, LIN, NV.PF_OBS_ACOUSTIC)
+    assert lib.pf_model_supported(5, 5, LIN, NV.PF_OBS_SV_EXACT)
+    assert not lib.pf_model_supported(5, 4, LIN, NV.PF_OBS_EXP_HALF)
+    assert M.supported(M.LinearTransition(np.eye(9)), M.BearingsObservation(9))
+    assert not M.compiled(M.LinearTransition(np.eye(9)), M.BearingsObservation(9))
+    assert M.kernel_path_code("runtime") == NV.PF_PATH_RUNTIME
+    with pytest.raises(ValueError):
+        M.kernel_path_code("jit")
+    st, _ = _create(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[1.0]], kernel_path=5)
+    assert st == NV.PF_E_ARG
+
+
+def test_bearings_observation_matches_notebook_formula():
+    h = M.BearingsObservation(9)
+    s = np.array([40.0, 40.0, 40.0, 8.0, 0.0, -3.0, 0.0, 0.0, 0.0])
+    r = np.sqrt(s[0] ** 2 + s[1] ** 2)
+    np.testing.assert_array_equal(h(s), [np.arctan2(s[0], s[1]), np.arctan2(s[2], r)])
 
 
 def test_status_exception_mapping():

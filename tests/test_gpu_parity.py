@@ -48,12 +48,15 @@ def device_models(name, ssm_case, sv, mat):
     raise KeyError(name)
 
 
-def run_engine(name, golden_sv, golden_l96, golden_mat, golden_runs, precision, steps=None):
+def run_engine(name, golden_sv, golden_l96, golden_mat, golden_runs, precision, steps=None, kernel_path="auto"):
     ssm, Z, controls, kw = pf_cases.build(name, golden_sv, golden_l96, golden_mat, golden_runs)
     g, h = device_models(name, ssm, golden_sv, golden_mat)
     pf = pfa.ParticleFilter(g, h, ssm.Q, ssm.R, Np=kw["Np"], resample_thresh=kw["thresh"],
                             resample_method=kw["method"], regularize_after_resample=kw["reg"],
-                            rng=np.random.default_rng(kw["seed"]), rng_mode="host", precision=precision)
+                            rng=np.random.default_rng(kw["seed"]), rng_mode="host", precision=precision,
+                            kernel_path=kernel_path)
+    if kernel_path == "runtime":
+        assert pf.kernel_path_used == "runtime"
     st0 = pf.initialize(np.asarray(kw["mean0"], float), np.asarray(kw["cov0"], float))
     init = st0.particles.copy()
     T = Z.shape[0] if steps is None else steps
