@@ -208,7 +208,38 @@ class MAT(Workload):
                 "synthetic (simulate_acoustic_dataset 4 targets seed=56 article init, R=0.01 I)")
 
 
-WORKLOADS = {"sv": SV, "sv64": SV64, "l96": L96, "mat": MAT, "ledh": None, "edh": None, "ledh_mat": None}
+class L96Big(L96):
+    """simulate_lorenz96's default dimension (nx = 1000, every 4th component observed): outside
+    the compiled shape list, so it runs on the runtime-shape kernels (csrc/pf_dyn.h)."""
+
+    name, n_particles, replicates, nx, nz = "l96_1000", 16_384, 1, 1000, 250
+    kernel_tmpl = "float,L96,LINEAR"
+    defaults = (50, 5)
+    cpu_steps = 1
+
+    def build(self, T, rank):
+        from particle_filters_amd import models as M, simulators as S
+
+        sim = S.simulate_lorenz96(nx=1000, F=8.0, dt=0.01, spinup_steps=1000, total_steps=T, Np=1,
+                                  obs_interval=1, obs_fraction=4, obs_error_std=1.0, seed=42)
+        Q = 0.1 ** 2 * np.eye(1000)
+        return (M.L96Transition(8.0, 0.01, 1000), M.SelectObservation(sim.H_idx, 1000), Q, sim.R,
+                sim.observations[1:], sim.truth_traj[1:], sim.ensemble_traj[0, 0], 2.0 * np.eye(1000))
+
+    def oracle_ssm(self):
+        from oracle import ssm_oracle
+
+        return ssm_oracle.lorenz96(nx=1000, q_std=0.1)
+
+    def describe(self, world):
+        return ("SIR bootstrap PF, Lorenz-96 d=1000 (simulate_lorenz96's default size; runtime-shape kernels): "
+                "RK4 dt=0.01 F=8, every 4th component observed (R=I), Q=0.01 I, N=16384 particles per GPU, "
+                "systematic resampling at Neff<0.5N",
+                "synthetic (simulate_lorenz96 nx=1000 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)")
+
+
+WORKLOADS = {"sv": SV, "sv64": SV64, "l96": L96, "l96_1000": L96Big, "mat": MAT, "ledh": None, "edh": None,
+             "ledh_mat": None}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector 157.3 TF of MI355X_MICROARCH.md)
 
 
@@ -537,6 +568,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
     ap.add_argument("--precision", choices=("fp32", "fp64"), default="fp32")
+    ap.add_argument("--kernel-path", choices=("auto", "runtime"), default="auto",
+                    help="runtime: run the model on the runtime-shape kernels even if its shape is compiled")
     ap.add_argument("--spawn", action="store_true", help="launch the rank processes even for --gpus 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref", action="store_true", help="skip the rmse_vs_ref oracle leg")
@@ -585,7 +618,7 @@ def main():
 
     dZw, dZ = dz(Zall[:W]), dz(Zall[W:W + K])
     pf = ParticleFilterBatch(g, h, Q, R, Np=Np, n_replicates=Rl, replicate_base=rank * Rl,
-                             seed=42, precision=args.precision, device=local)
+                             seed=42, precision=args.precision, device=local, kernel_path=args.kernel_path)
     pf.initialize(mean0, cov0)
     lib = NV.load()
     NV.check(lib.pf_set_timing(pf.handle, 1), "pf_set_timing")
@@ -680,7 +713,12 @@ def main():
     base_b, res_b = 2 * esz * nx + 2 * esz, 2 * esz * nx + 12.0  # SURVEY.md 8(d) at the storage width
     alg_bytes_run = Np * (K * Rl * base_b + float(local_flags.sum()) * res_b)
     achieved = alg_bytes_run / (device_ms * 1e-3) / 1e9
-    kname = "k_resident" if resident else ("k_step_grp" if nx >= 16 else "k_step")  # large states: group kernel
+    dyn = lib.pf_kernel_path(pf.handle) == NV.PF_PATH_RUNTIME
+    # large states: group kernel; shapes outside the compiled list: the runtime-shape kernel
+    kname = "k_resident" if resident else ("k_dyn_step" if dyn else ("k_step_grp" if nx >= 16 else "k_step"))
+    ktmpl = wl.kernel_tmpl.split(",", 1)[1]
+    if dyn:
+        ktmpl = ",".join(ktmpl.split(",")[-2:])  # k_dyn_step<Real, TK, OK>
     traffic, traffic_src = pmc_traffic(wl.name, kname)
     G, tile, lds = pf.geometry()
     workload_desc, data_desc = wl.describe(world)
@@ -735,6 +773,7 @@ def main():
             "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": data_desc,
             "config": {"workload": workload_desc, "n_particles": Np, "replicates_per_gpu": Rl,
+                       "kernel_path": "runtime-shape (pf_dyn.h)" if dyn else "compiled shape",
                        "parallelism": f"replicates x{world} (independent filters per GPU"
                                       + (", RCCL all-gather of summaries)" if dist else ")"),
                        "geometry": {"tiles": G, "tile": tile, "lds_bytes": lds}},
@@ -744,7 +783,7 @@ def main():
             "resample_rate": resample_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"pf::{kname}<{real},{wl.kernel_tmpl.split(',', 1)[1]}>",
+                         "kernel": f"pf::{kname}<{real},{ktmpl}>",
                          "steps_per_launch": K if resident else 1,
                          "algorithmic_bytes_per_step": alg_bytes_run / K,
                          "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),

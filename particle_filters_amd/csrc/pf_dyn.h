@@ -573,7 +573,8 @@ __global__ void __launch_bounds__(DBS) k_dyn_head(StepParams p, double* head) {
 template <typename Real>
 __global__ void __launch_bounds__(DBS) k_dyn_init(Real* x, double* rec, const Real* mean, const Real* Lc,
                                                   const double* replay, int64_t N, int64_t Npad, int G, uint64_t seed,
-                                                  uint32_t epoch, int rep_base, int64_t pbase, int nx) {
+                                                  uint32_t epoch, int rep_base, int64_t pbase, int nx,
+                                                  int lc_diag) {
   const DynRec RC(nx);
   const int r = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * DBS + threadIdx.x;
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(DBS) k_dyn_init(Real* x, double* rec, const Re
     const Real* L = Lc + (int64_t)r * nx * nx;
     for (int d = nx - 1; d >= 0; --d) {
       Real acc = Real(0);
-      for (int e = 0; e <= d; ++e) acc += xc[e * Npad] * L[d * nx + e];
+      for (int e = lc_diag ? d : 0; e <= d; ++e) acc += xc[e * Npad] * L[d * nx + e];  // (zeros add exactly)
       xc[d * Npad] = acc + mean[r * nx + d];
     }
   }

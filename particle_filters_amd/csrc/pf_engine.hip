@@ -930,8 +930,13 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   }
   if (!st) {
     const uint32_t ep = h->epoch++;
+    int lc_diag = 1;  // every replicate's factor diagonal: the runtime-shape init skips the zeros
+    for (int r = 0; r < R && lc_diag; ++r)
+      for (int i = 0; i < nx && lc_diag; ++i)
+        for (int j = 0; j < i; ++j)
+          if (Lc[(size_t)r * nx * nx + i * nx + j] != 0.0) { lc_diag = 0; break; }
     hipError_t e = h->ops->init(h->x[h->cx ^ 1], h->rec[h->crec ^ 1], dmean, dL, drep, h->N, h->Npad, h->G, R,
-                                h->seed, ep, h->rep_base, h->pbase, h->stream, nx);
+                                h->seed, ep, h->rep_base, h->pbase, h->stream, nx, lc_diag);
     if (e != hipSuccess) st = fail(PF_E_HIP, std::string("init launch: ") + hipGetErrorString(e));
     h->cx ^= 1;
     h->crec ^= 1;

@@ -26,11 +26,11 @@ struct DynLaunch {
   }
   static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay, int64_t N,
                          int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, int64_t pbase,
-                         hipStream_t s, int nx) {
+                         hipStream_t s, int nx, int lc_diag) {
     const int64_t n = N > G ? N : G;
     dim3 grid((unsigned)((n + DBS - 1) / DBS), (unsigned)R);
     hipLaunchKernelGGL((k_dyn_init<Real>), grid, dim3(DBS), 0, s, (Real*)x, rec, (const Real*)mean, (const Real*)Lc,
-                       replay, N, Npad, G, seed, epoch, rep_base, pbase, nx);
+                       replay, N, Npad, G, seed, epoch, rep_base, pbase, nx, lc_diag);
     return hipGetLastError();
   }
   static hipError_t moments(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,

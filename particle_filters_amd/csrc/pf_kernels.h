@@ -41,7 +41,10 @@ namespace pf {
 
 constexpr int BLOCK = 256;
 constexpr int NWAVES = BLOCK / 64;
-constexpr int MAXG = 1024;         // tiles per replicate
+#ifndef PF_MAXG
+#define PF_MAXG 1024
+#endif
+constexpr int MAXG = PF_MAXG;      // tiles per replicate
 
 // Diagnostic phase stamps (PF_STAMPS builds only; never in the product library):
 // per workgroup, thread 0 records s_memrealtime (100 MHz) at phase boundaries.

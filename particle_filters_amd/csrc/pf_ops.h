@@ -28,7 +28,7 @@ struct Ops {
   hipError_t (*head)(const StepParams&, double* head_out, dim3, size_t, hipStream_t);
   hipError_t (*init)(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                      int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch, int rep_base, int64_t pbase,
-                     hipStream_t, int nx);
+                     hipStream_t, int nx, int lc_diag);
   hipError_t (*moments)(const void* x, const void* lw, const double* rec, int G, const double* lse, int64_t N,
                         int64_t Npad, int R, double* mean, double* cov, hipStream_t, int nx);
   void (*prepare)();  // per-device kernel attributes, called once a device is current
@@ -79,7 +79,7 @@ struct Launch {
   }
   static hipError_t init(void* x, double* rec, const void* mean, const void* Lc, const double* replay,
                          int64_t N, int64_t Npad, int G, int R, uint64_t seed, uint32_t epoch,
-                         int rep_base, int64_t pbase, hipStream_t s, int) {
+                         int rep_base, int64_t pbase, hipStream_t s, int, int) {
     const int64_t n = N > G ? N : G;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK), (unsigned)R);
     hipLaunchKernelGGL((k_init<Real, NX>), grid, dim3(BLOCK), 0, s, (Real*)x, rec, (const Real*)mean,

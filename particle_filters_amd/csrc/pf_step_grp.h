@@ -19,6 +19,15 @@
 
 namespace pf {
 
+#ifndef PF_GRP_WPE
+#define PF_GRP_WPE 4
+#endif
+#ifndef PF_GRP_WPE_SMALL
+#define PF_GRP_WPE_SMALL 4
+#endif
+#ifndef PF_GRP_RCP
+#define PF_GRP_RCP 1
+#endif
 constexpr int SYS_STAGE = 4;  // source tiles of a block's systematic positions staged in LDS (sys_cdf)
 
 template <int NX>
@@ -185,7 +194,12 @@ __device__ __forceinline__ Real grp_loglik(const Real* x, const Real* z, const R
 #pragma unroll
       for (int c = 0; c < SGL * TPL; ++c) {
         const Real dx = px[c] - sx, dy = py[c] - sy;
-        zp += psi / ((dx * dx + dy * dy) + d0);
+#if PF_GRP_RCP
+        if constexpr (sizeof(Real) == 4)  // fp32 engine: v_rcp_f32 (1 ulp) instead of the IEEE division sequence
+          zp += psi * __builtin_amdgcn_rcpf((dx * dx + dy * dy) + d0);
+        else
+#endif
+          zp += psi / ((dx * dx + dy * dy) + d0);
       }
       const Real y = ylin(k, zp);
       quad += y * y;
@@ -365,7 +379,7 @@ struct GAcc {
 // The fp32 L96-size variant with diagonal R and lane-local noise fits 128 VGPRs: keep
 // it at 4 waves per SIMD (the others need more registers than that).
 template <typename Real, int NX, int NZ, int TK, int OK, bool RD, bool QL>
-constexpr int grp_waves_per_eu = (sizeof(Real) == 4 && RD && QL && NX >= 32) ? 4 : 1;
+constexpr int grp_waves_per_eu = (sizeof(Real) == 4 && RD && QL) ? (NX >= 32 ? PF_GRP_WPE : PF_GRP_WPE_SMALL) : 1;
 
 template <typename Real, int NX, int NZ, int TK, int OK, bool RD, bool QL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu<Real, NX, NZ, TK, OK, RD, QL>)))
