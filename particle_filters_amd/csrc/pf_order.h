@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 
 namespace pf {
@@ -20,14 +21,21 @@ inline GridOrder& grid_order() {
   static GridOrder o;  // one per process (inline function: shared by every translation unit)
   return o;
 }
+inline bool grid_order_off() {  // PF_NO_ORDER=1: diagnostics only (unsafe with several handles)
+  static const bool off = [] {
+    const char* e = std::getenv("PF_NO_ORDER");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
 inline void grid_order_begin(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64) return;
+  if (dev < 0 || dev >= 64 || grid_order_off()) return;
   GridOrder& o = grid_order();
   std::lock_guard<std::mutex> lk(o.mu);
   if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
 }
 inline void grid_order_end(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64) return;
+  if (dev < 0 || dev >= 64 || grid_order_off()) return;
   GridOrder& o = grid_order();
   std::lock_guard<std::mutex> lk(o.mu);
   if (!o.ev[dev] && hipEventCreateWithFlags(&o.ev[dev], hipEventDisableTiming) != hipSuccess) {
