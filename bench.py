@@ -568,6 +568,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sv")
     ap.add_argument("--precision", choices=("fp32", "fp64"), default="fp32")
+    ap.add_argument("--replicates-total", type=int, default=None,
+                    help="strong scaling: this many replicates over all ranks (SURVEY 8(e): R=64 for MAT); "
+                         "default: the workload's fixed replicates per GPU (weak scaling)")
     ap.add_argument("--kernel-path", choices=("auto", "runtime"), default="auto",
                     help="runtime: run the model on the runtime-shape kernels even if its shape is compiled")
     ap.add_argument("--spawn", action="store_true", help="launch the rank processes even for --gpus 1")
@@ -609,6 +612,15 @@ def main():
     T_data = W + max(K, cpu_need)
     g, h, Q, R, Zall, truth_all, mean0, cov0 = wl.build(T_data, rank)
     nx, Rl, Np = wl.nx, wl.replicates, wl.n_particles
+    strong = args.replicates_total is not None
+    rbase = rank * Rl
+    if strong:  # distributed.shard_replicates: rank r runs a contiguous block of the global replicates
+        from particle_filters_amd.distributed import shard_replicates
+
+        if args.replicates_total % world:  # the summaries' all-gather takes equal blocks per rank
+            raise SystemExit(f"--replicates-total {args.replicates_total} is not a multiple of {world} ranks")
+        rbase, Rl = shard_replicates(args.replicates_total, world, rank)
+        wl.replicates = Rl
     dev = torch.device("cuda", local)
     rdt = torch.float32 if args.precision == "fp32" else torch.float64
 
@@ -620,7 +632,7 @@ def main():
     # gather buffers are the same allocations (the same pages) the warm-up already ran on
     dZall = dz(Zall[:W + K])
     dZw, dZ = dZall[:W], dZall[W:W + K]
-    pf = ParticleFilterBatch(g, h, Q, R, Np=Np, n_replicates=Rl, replicate_base=rank * Rl,
+    pf = ParticleFilterBatch(g, h, Q, R, Np=Np, n_replicates=Rl, replicate_base=rbase,
                              seed=42, precision=args.precision, device=local, kernel_path=args.kernel_path)
     pf.initialize(mean0, cov0)
     lib = NV.load()
@@ -777,11 +789,12 @@ def main():
             "warmup": W,
             "ms_per_step": elapsed * 1e3 / K,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": data_desc,
             "config": {"workload": workload_desc, "n_particles": Np, "replicates_per_gpu": Rl,
+                       "replicates_total": Rl * world,
                        "kernel_path": "runtime-shape (pf_dyn.h)" if dyn else "compiled shape",
                        "parallelism": f"replicates x{world} (independent filters per GPU"
                                       + (", RCCL all-gather of summaries)" if dist else ")"),

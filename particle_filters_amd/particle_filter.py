@@ -28,6 +28,9 @@ Differences a user sees:
   carries the per-tile W2 / moment sums as fp32 (the tile mass S0 as fp64), so its
   Neff decision and moments are fp32-reduced per tile.
 * ``state`` arrays live on the GPU and are fetched lazily on attribute access.
+* Any (nx, nz): shapes in the compiled list keep the particle in registers; any other shape
+  (or ``kernel_path="runtime"``) runs the runtime-shape kernels (``csrc/pf_dyn.h``);
+  ``kernel_path_used`` says which.
 """
 
 from __future__ import annotations
