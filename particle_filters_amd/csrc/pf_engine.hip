@@ -786,7 +786,8 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
           if (i / per != j / per && P[off + i * nx + j] != 0.0) return 0;
       return 1;
     };
-    h->lq_local = local(lay_LQ);
+    // a linear g's A joins the chol(Q) test: the lane-local variant also applies A within the blocks
+    h->lq_local = local(lay_LQ) && (m->trans_kind != PF_TRANS_LINEAR || local(lay_A));
     h->lj_local = local(lay_LJ);
   }
   for (int c = 0; c < 64; ++c) h->hcol2k[c] = -1;

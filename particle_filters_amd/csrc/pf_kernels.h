@@ -50,11 +50,13 @@ constexpr int MAXG = PF_MAXG;      // tiles per replicate
 // per workgroup, thread 0 records s_memrealtime (100 MHz) at phase boundaries.
 #ifdef PF_STAMPS
 constexpr int STAMP_SLOTS = 10;
-__device__ unsigned long long g_pf_stamps[4096 * STAMP_SLOTS];
-#define PF_STAMP(k)                                                                     \
-  do {                                                                                  \
-    if (stamp_on && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4096)            \
-      g_pf_stamps[blockIdx.x * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime();    \
+constexpr int STAMP_WG = 65536;  // workgroups stamped: linear id y * gridDim.x + x (replicate-major)
+__device__ unsigned long long g_pf_stamps[STAMP_WG * STAMP_SLOTS];
+#define PF_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    const unsigned wid_ = blockIdx.y * gridDim.x + blockIdx.x;                                          \
+    if (stamp_on && threadIdx.x == 0 && wid_ < (unsigned)STAMP_WG)                                      \
+      g_pf_stamps[wid_ * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime();                         \
   } while (0)
 #else
 #define PF_STAMP(k) \
@@ -656,8 +658,14 @@ constexpr int LDS_RED = 512;
 constexpr int LDS_PL = LDS_RED;
 __host__ __device__ constexpr int lds_tile(int G) { return LDS_PL + ((G + 8) & ~7); }
 
+// waves per SIMD the scalar-state step is compiled for (its VGPR cap; LDS allows 5 workgroups
+// per CU with the gather area of a 2048-particle tile)
+#ifndef PF_STEP_WPE
+#define PF_STEP_WPE 4
+#endif
 template <typename Real, int NX, int NZ, int TK, int OK>
-__global__ void __launch_bounds__(step_bs<NX>) k_step(StepParams p) {
+__global__ void __launch_bounds__(step_bs<NX>) __attribute__((amdgpu_waves_per_eu(NX == 1 ? PF_STEP_WPE : 1)))
+k_step(StepParams p) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
   using WA = WAcc<Real, NX>;

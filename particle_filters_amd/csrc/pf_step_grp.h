@@ -108,7 +108,9 @@ __device__ __forceinline__ void grp_add_lower(Real* x, const Real* n, const Real
   for (int j = 0; j < PER; ++j) x[j] = x[j] + acc[j];
 }
 
-template <typename Real, int NX, int NZ, int TK>
+// LOCAL: A is block-diagonal in the lanes' blocks (the joint MAT model's per-target constant-
+// velocity blocks): each lane applies its own PER x PER block, no shuffles
+template <typename Real, int NX, int NZ, int TK, bool LOCAL>
 __device__ __forceinline__ void grp_transition(Real* x, const Real* __restrict__ P, const Real* u, int q, int base) {
   using L = ParamLayout<NX, NZ>;
   constexpr int PER = SGrp<NX>::PER, SGL = SGrp<NX>::GL;
@@ -116,7 +118,14 @@ __device__ __forceinline__ void grp_transition(Real* x, const Real* __restrict__
     Real y[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) y[j] = Real(0);
-    grp_rows<Real, NX>(x, P + L::A, q, base, y, false);
+    if constexpr (LOCAL) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+#pragma unroll
+        for (int jj = 0; jj < PER; ++jj) y[j] += P[L::A + (q * PER + j) * NX + q * PER + jj] * x[jj];
+    } else {
+      grp_rows<Real, NX>(x, P + L::A, q, base, y, false);
+    }
 #pragma unroll
     for (int j = 0; j < PER; ++j) x[j] = u ? y[j] + u[q * PER + j] : y[j];
   } else {  // L96 RK4 (simulator_Lorenz_96.py:62-84), neighbours across lanes by shuffles
@@ -374,8 +383,8 @@ struct GAcc {
   }
 };
 
-// RD: R diagonal (the likelihood streams over k); QL: chol(Q) and the jitter factor are
-// block-diagonal in the lanes' blocks (noise is lane-local).  Variants picked on the host.
+// RD: R diagonal (the likelihood streams over k); QL: chol(Q), the jitter factor and (linear g)
+// A are block-diagonal in the lanes' blocks (noise and transition are lane-local).  Variants picked on the host.
 // The fp32 L96-size variant with diagonal R and lane-local noise fits 128 VGPRs: keep
 // it at 4 waves per SIMD (the others need more registers than that).
 template <typename Real, int NX, int NZ, int TK, int OK, bool RD, bool QL>
@@ -449,9 +458,16 @@ k_step_grp(StepParams p) {
         return (mk > -INFINITY) ? exp(mk - h.M) / h.Sscan : 0.0;
       };
       __shared__ int krange[2];
-      if (t == 0) {
-        krange[0] = prefix_tile(Pl, p.G, (U + (double)o0) / (double)p.N);
-        krange[1] = prefix_tile(Pl, p.G, (U + (double)(o1 - 1)) / (double)p.N);
+      __shared__ double cks[SYS_STAGE];  // c_k of the staged source tiles (one fp64 exp per tile)
+      if (t < 64) {  // wave 0: the first and last source tile by two lanes at once, then their c_k
+        int kk = 0;
+        if (lane < 2) kk = prefix_tile(Pl, p.G, (U + (double)(lane == 0 ? o0 : o1 - 1)) / (double)p.N);
+        const int klo_ = __shfl(kk, 0), khi_ = __shfl(kk, 1);
+        if (lane == 0) {
+          krange[0] = klo_;
+          krange[1] = khi_;
+        }
+        if (Lc && lane < SYS_STAGE && klo_ + lane <= khi_) cks[lane] = ck(klo_ + lane);
       }
       __syncthreads();
       const int klo = krange[0], nk = krange[1] - krange[0] + 1;
@@ -461,8 +477,8 @@ k_step_grp(StepParams p) {
         for (int e = t; e < nk * p.tile; e += BS) {
           const int64_t g = (int64_t)klo * p.tile + e;
           if (Lc) {
-            const int k = klo + e / p.tile;
-            stg[e] = g < p.N ? Pl[k] + ck(k) * Lc[g] : INFINITY;
+            const int kq = e / p.tile;
+            stg[e] = g < p.N ? Pl[klo + kq] + cks[kq] * Lc[g] : INFINITY;
           } else {
             stg[e] = g < p.N ? C[g] : INFINITY;
           }
@@ -587,7 +603,7 @@ k_step_grp(StepParams p) {
       } else {
         grp_normals<Real, PER>(p.seed, (i + p.pbase) * NX + q * PER, rep, p.ep_predict, STREAM_PROCESS, n);
       }
-      grp_transition<Real, NX, NZ, TK>(x, P, u, q, base);
+      grp_transition<Real, NX, NZ, TK, QL>(x, P, u, q, base);
       grp_add_lower<Real, NX, QL>(x, n, P, M::L::LQ, q, base);
     }
     if (p.do_update) {

@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../particle_filters_amd/csrc"
 B=../../build/csrc
-OTHERS="$B/pf_diag.o $B/pf_engine.o $B/pf_inst_linear.o $B/pf_inst_l96.o $B/pf_inst_mat.o $B/pf_ledh.o"
+OTHERS="$B/pf_diag.o $B/pf_engine.o $B/pf_inst_linear.o $B/pf_inst_l96.o $B/pf_inst_mat.o $B/pf_inst_dyn.o $B/pf_ledh.o"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-pass-failed $flags \
