@@ -206,6 +206,71 @@ __device__ __forceinline__ double wave_max_ud(double v) {
   return lane63_d(v);
 }
 
+// Inclusive wave scan on the DPP network (row_shr 1/2/4/8 within 16-lane rows, then the row
+// broadcasts): no LDS crossbar round trips.  A fixed order, identical in every workgroup.
+__device__ __forceinline__ double wave_incl_scan_dpp(double v) {
+  v += dpp_d<0x111>(0.0, v);  // row_shr:1
+  v += dpp_d<0x112>(0.0, v);  // row_shr:2
+  v += dpp_d<0x114>(0.0, v);  // row_shr:4
+  v += dpp_d<0x118>(0.0, v);  // row_shr:8
+  v += dpp_d<DPP_ROW_BCAST15, 0xa>(0.0, v);
+  v += dpp_d<DPP_ROW_BCAST31, 0xc>(0.0, v);
+  return v;
+}
+
+// The prologue's block reductions on the DPP network (uniform wave results, no LDS-crossbar
+// shuffles; a fixed combination tree, identical in every workgroup and every kernel that
+// reduces a replicate's records: k_step, k_step_grp, k_cdf, k_head, k_finalize, k_dyn_*).
+template <int BS>
+__device__ __forceinline__ double pblock_max(double v, double* red) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max_ud(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) s = fmax(s, red[i]);
+  return s;
+}
+template <int K, int BS>
+__device__ __forceinline__ void pblock_sum_k(double (&v)[K], double* red) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < K; ++i) v[i] = wave_sum_ud(v[i]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < K; ++i) red[w * K + i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double s = red[i];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) s += red[j * K + i];
+    v[i] = s;
+  }
+}
+template <int BS>
+__device__ __forceinline__ double pblock_excl_scan(double v, double* red, double* total) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double incl = wave_incl_scan_dpp(v);
+  __syncthreads();
+  if (lane == 63) red[w] = incl;
+  __syncthreads();
+  double off = 0.0, tot = 0.0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    if (i < w) off += red[i];
+    tot += red[i];
+  }
+  *total = tot;
+  return off + incl - v;
+}
+
 // Block reductions (BS threads) over K values at once; `red` needs (BS/64)*K doubles.
 template <int K, int BS = BLOCK>
 __device__ __forceinline__ void block_sum_k(double (&v)[K], double* red) {
@@ -380,7 +445,7 @@ __device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, do
 #pragma unroll
   for (int j = 0; j < RPT; ++j)
     if (s0k[j] > 0.0) lmax = fmax(lmax, mk[j]);
-  const double M = block_max<BS>(lmax, red);
+  const double M = pblock_max<BS>(lmax, red);
   double s[2] = {0.0, 0.0};
   double wk[RPT];
 #pragma unroll
@@ -391,7 +456,7 @@ __device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, do
     s[1] += s00k[j] * f * f;
   }
   const double tsum = s[0];
-  block_sum_k<2, BS>(s, red);
+  pblock_sum_k<2, BS>(s, red);
   h.M = M;
   h.S = s[0];
   h.S2 = s[1];
@@ -401,7 +466,7 @@ __device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, do
   h.resample = allow && (force || h.neff < thresh * (double)N);
   if (want_prefix && h.resample) {  // normalised exclusive prefix of the tile weights
     double S;
-    double run = block_excl_scan<BS>(tsum, red, &S);
+    double run = pblock_excl_scan<BS>(tsum, red, &S);
     h.Sscan = S;
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
@@ -555,6 +620,47 @@ __device__ __forceinline__ int tile_cdf(const Real* __restrict__ lw, const doubl
     off += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
     cdf[j] = base + c * off;
   }
+  __syncthreads();
+  return len;
+}
+
+// tile_cdf from log-weights the caller already holds in registers (thread t: elements
+// [t per, t per + per) of tile k, loaded one source tile ahead by load_tile_lw): the same
+// partition, exponentials and summation order, so exactly tile_cdf's doubles
+template <typename Real, int PM>
+__device__ __forceinline__ void load_tile_lw(const Real* __restrict__ lw, int64_t N, int tile, int k, int BS,
+                                             Real (&lv)[PM]) {
+  const int64_t s = (int64_t)k * tile;
+  const int len = (int)min((int64_t)tile, N - s);
+  const int per = (len + BS - 1) / BS;
+  const int j0 = threadIdx.x * per;
+#pragma unroll
+  for (int q = 0; q < PM; ++q)
+    if (q < per && j0 + q < len) lv[q] = lw[s + j0 + q];
+}
+template <typename Real, int NX, int BS, int PM>
+__device__ __forceinline__ int tile_cdf_regs(const Real (&lv)[PM], const double* rec, int G, int64_t N, int tile, int k,
+                                             const Head& h, const double* Pl, double* cdf, double* red) {
+  const int64_t s = (int64_t)k * tile;
+  const int len = (int)min((int64_t)tile, N - s);
+  const int per = (len + BS - 1) / BS;
+  const int j0 = threadIdx.x * per;
+  const double mk = rec[Rec<NX>::M * G + k];
+  const Real m = (Real)mk;
+  double acc = 0.0;
+#pragma unroll
+  for (int q = 0; q < PM; ++q)
+    if (q < per && j0 + q < len) acc += (lv[q] > -INFINITY) ? (double)exp_r<Real>(lv[q] - m) : 0.0;
+  double tot;
+  double off = block_excl_scan<BS>(acc, red, &tot);
+  const double c = (mk > -INFINITY) ? exp(mk - h.M) / h.Sscan : 0.0;
+  const double base = Pl[k];
+#pragma unroll
+  for (int q = 0; q < PM; ++q)
+    if (q < per && j0 + q < len) {
+      off += (lv[q] > -INFINITY) ? (double)exp_r<Real>(lv[q] - m) : 0.0;
+      cdf[j0 + q] = base + c * off;
+    }
   __syncthreads();
   return len;
 }
@@ -748,13 +854,13 @@ constexpr int LDS_RED = 512;
 constexpr int LDS_PL = LDS_RED;
 __host__ __device__ constexpr int lds_tile(int G) { return LDS_PL + ((G + 8) & ~7); }
 
-// waves per SIMD the scalar-state step is compiled for (its VGPR cap; LDS allows 5 workgroups
+// waves per SIMD the fp32 scalar-state step is compiled for (its VGPR cap; LDS allows 5 workgroups
 // per CU with the gather area of a 2048-particle tile)
 #ifndef PF_STEP_WPE
 #define PF_STEP_WPE 4
 #endif
 template <typename Real, int NX, int NZ, int TK, int OK>
-__global__ void __launch_bounds__(step_bs<NX>) __attribute__((amdgpu_waves_per_eu(NX == 1 ? PF_STEP_WPE : 1)))
+__global__ void __launch_bounds__(step_bs<NX>) __attribute__((amdgpu_waves_per_eu((NX == 1 && sizeof(Real) == 4) ? PF_STEP_WPE : 1)))
 k_step(StepParams p) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
@@ -881,8 +987,24 @@ k_step(StepParams p) {
         }
       }
       int k = block_min_i<BS>(nextk, red);
+      // source tiles of <= 8 log-weights per thread: each tile's log-weights are loaded one tile
+      // ahead (the likeliest next source tile is k + 1), in flight through the current tile's
+      // searches, and read once (tile_cdf_regs) instead of twice from memory
+      constexpr int PM = sizeof(Real) == 4 ? 8 : 1;  // fp64: the 16 extra VGPRs would spill
+      const bool regs = PM > 1 && (p.tile + BS - 1) / BS <= PM;
+      Real lv[PM];
+      int kl = -1;
+      if (regs && k < p.G) {
+        load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k, BS, lv);
+        kl = k;
+      }
       while (k < p.G) {
-        const int len = tile_cdf<Real, NX, BS>(lw_in, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red);
+        const int len = regs ? tile_cdf_regs<Real, NX, BS, PM>(lv, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red)
+                             : tile_cdf<Real, NX, BS>(lw_in, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red);
+        if (regs && k + 1 < p.G) {
+          load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k + 1, BS, lv);
+          kl = k + 1;
+        }
         nextk = p.G;
         for (int c = t; c < nchunks; c += BS) {
 #pragma unroll
@@ -900,6 +1022,10 @@ k_step(StepParams p) {
         }
         __syncthreads();  // the tile CDF is rebuilt for the next tile
         k = block_min_i<BS>(nextk, red);
+        if (regs && k < p.G && k != kl) {
+          load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k, BS, lv);
+          kl = k;
+        }
       }
     } else {  // multinomial: binary search of the materialised CDF (cdf /= cdf[-1])
       const double* C = p.cdf + (int64_t)r * p.N;

@@ -297,18 +297,6 @@ __device__ __forceinline__ int count_below(double x, double U, int N) {
   return count_below_exact(x, U, N, c);
 }
 
-// Inclusive wave scan on the DPP network (row_shr 1/2/4/8 within 16-lane rows, then the row
-// broadcasts): no LDS crossbar round trips.  A fixed order, identical in every workgroup.
-__device__ __forceinline__ double wave_incl_scan_dpp(double v) {
-  v += dpp_d<0x111>(0.0, v);  // row_shr:1
-  v += dpp_d<0x112>(0.0, v);  // row_shr:2
-  v += dpp_d<0x114>(0.0, v);  // row_shr:4
-  v += dpp_d<0x118>(0.0, v);  // row_shr:8
-  v += dpp_d<DPP_ROW_BCAST15, 0xa>(0.0, v);
-  v += dpp_d<DPP_ROW_BCAST31, 0xc>(0.0, v);
-  return v;
-}
-
 // Two exclusive block scans in one pass (one pair of barriers): returns a's exclusive prefix,
 // *tot_a / *tot_b the totals, *excl_b b's exclusive prefix.  red >= 2 * BS / 64 doubles.
 template <int BS>

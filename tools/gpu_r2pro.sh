@@ -1,0 +1,14 @@
+#!/bin/bash
+# DPP prologue reductions: GPU suite, then A/B against the previous library (L96, fp64 SV, sv64, MAT)
+D=gpurun_out/r2pro
+mkdir -p $D
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1
+rc=$?; echo "tests rc=$rc" >> $D/steps.log; [ $rc -ne 0 ] && exit $rc
+for v in prev new prev2 new2; do
+  lib=particle_filters_amd/libpf_hip.so; [ ${v#prev} != $v ] && lib=build/libpf_hip_prev.so
+  PF_LIB=$lib timeout -k 10 200 python -u bench.py --workload l96 --steps 100 --warmup 10 --no-cpu-baseline --no-ref > $D/l96_$v.json 2>/dev/null
+  PF_LIB=$lib timeout -k 10 200 python -u bench.py --precision fp64 --steps 200 --warmup 5 --no-cpu-baseline --no-ref > $D/fp64_$v.json 2>/dev/null
+  PF_LIB=$lib timeout -k 10 200 python -u bench.py --workload mat --steps 50 --warmup 5 --no-cpu-baseline --no-ref > $D/mat_$v.json 2>/dev/null
+  PF_LIB=$lib timeout -k 10 200 python -u bench.py --workload sv64 --steps 50 --warmup 3 --no-cpu-baseline --no-ref > $D/sv64_$v.json 2>/dev/null
+  echo "$v rc=$?" >> $D/steps.log
+done
