@@ -64,11 +64,16 @@ struct Normal4 {
 
 // Box-Muller on the two pairs (x, y) and (z, w): r = sqrt(-2 ln u1), angle 2*pi*u2.
 // fp32: the hardware v_sin/v_cos (argument in revolutions, so 2*pi*u2 needs no
-// range reduction), v_log and v_sqrt — a handful of instructions per pair.
+// range reduction), v_log and v_sqrt — a handful of instructions per pair.  u1 is a
+// normal float in [2^-24, 1], so the radius takes the raw v_log_f32 (log2, 1 ulp) times
+// 2 ln 2 — no denormal rescaling and no compensated ln2 product (__logf's 10 instructions).
+__device__ __forceinline__ float neg2_ln_u01(uint32_t a) {
+  return -1.3862943611198906f * __builtin_amdgcn_logf(u01_f32(a));  // -2 ln u = -2 ln2 log2 u
+}
 __device__ __forceinline__ Normal4<float> box_muller4(u32x4 r) {
   Normal4<float> n;
-  const float r0 = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_f32(r.x)));
-  const float r1 = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_f32(r.z)));
+  const float r0 = __builtin_amdgcn_sqrtf(neg2_ln_u01(r.x));
+  const float r1 = __builtin_amdgcn_sqrtf(neg2_ln_u01(r.z));
   const float a0 = (float)(r.y >> 8) * (1.0f / 16777216.0f);
   const float a1 = (float)(r.w >> 8) * (1.0f / 16777216.0f);
   n.v[0] = r0 * __builtin_amdgcn_cosf(a0);
