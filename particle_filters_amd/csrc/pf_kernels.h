@@ -800,7 +800,8 @@ struct WAcc {
     // wave partials on the DPP network (row reductions + row broadcasts, lane 63 read back as a
     // uniform value): no LDS-crossbar shuffles on the record's critical path
     const double md = (double)m;
-    const double Mw = wave_max_ud(md);
+    // fp32 engine: the maxima are floats, so the fp32 DPP max is the same value in fewer issues
+    const double Mw = sizeof(Real) == 4 ? (double)wave_max_u((float)m) : wave_max_ud(md);
     const double f = (md > -INFINITY) ? exp(md - Mw) : 0.0;
     double v[NS];
 #pragma unroll
@@ -815,7 +816,7 @@ struct WAcc {
     if (w != 0) return;
     // wave 0: lane j < NW holds wave j's partial; one exp per lane, then DPP sums
     const double mj = lane < NW ? red[lane * (NS + 1)] : -INFINITY;
-    const double M = wave_max_ud(mj);
+    const double M = sizeof(Real) == 4 ? (double)wave_max_u((float)mj) : wave_max_ud(mj);
     const double fj = (mj > -INFINITY) ? exp(mj - M) : 0.0;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {

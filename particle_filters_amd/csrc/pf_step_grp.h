@@ -336,7 +336,9 @@ struct GAcc {
     constexpr int NW = BS / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane % SGL;
     const double md = (double)m;
-    const double Mw = wave_max(md);
+    // the lane maxima are Real values: for fp32 the DPP max of the floats (the same value as the
+    // shuffle butterfly over their doubles, without the LDS-crossbar round trips)
+    const double Mw = sizeof(Real) == 4 ? (double)wave_max_u((float)m) : wave_max(md);
     const double f = (md > -INFINITY) ? exp(md - Mw) : 0.0;
     double v0 = (double)s0 * f, v1 = (double)s00 * f * f, vj[PER];
 #pragma unroll
