@@ -497,6 +497,12 @@ def rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, eng_means, eng_flags, pr
     PhiloxSIROracle on a bounded number of steps."""
     from oracle import sir_philox as SP
 
+    if wl.nx > 1:  # the NumPy oracle runs from initialize: a bounded window of the timed steps
+        K = min(K, int(3e8 // (wl.n_particles * wl.nx)) - W)
+        if K < 5:
+            return {"skipped": f"W={W} warm-up steps x N={wl.n_particles} x nx={wl.nx} exceed the NumPy oracle budget"}
+        eng_means = np.asarray(eng_means, float)[:K]
+        eng_flags = np.asarray(eng_flags)[:K]
     T = W + K
     truth = np.asarray(truth_all[W:T], float).reshape(K, -1)
     bm24 = precision == "fp32"
@@ -509,8 +515,6 @@ def rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, eng_means, eng_flags, pr
         om, of = o["means"][W:T, None], o["flags"][W:T]
         impl = f"oracle/sir_philox.c (fp64, {oracle_threads()} OpenMP threads)"
     else:
-        if T * wl.n_particles * wl.nx > 4e8:
-            return {"skipped": f"T={T} steps x N={wl.n_particles} x nx={wl.nx} exceeds the NumPy oracle budget"}
         from oracle import pf_oracle
         ssm = wl.oracle_ssm()
         o = SP.PhiloxSIROracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, seed=42, rep=0, bm24=bm24, Np=wl.n_particles,
