@@ -254,6 +254,23 @@ bool choose_geometry(pf_handle* h) {
   // reduces all G records of its replicate in the prologue: O(G^2 R) record reads)
   while (!env && (int64_t)h->R * ((h->N + tile - 1) / tile) > 4096 && tile < 256 && tile * 2 <= h->ops->tile_max)
     tile *= 2;
+  // large-state lane-group step (fp32, diagonal R, lane-local noise: 4 workgroups per CU, 1024
+  // resident on the 256 CUs) over many replicates: the R x G grid runs in rounds of 1024 and a
+  // workgroup's time is its chunk passes plus a fixed part (prologue / head, ancestors, record:
+  // ~1.5 passes), so take the passes per tile (<= 8) that minimise rounds x (passes + 1.5).
+  // MAT 8 x 1e5: 256 -> 448 (3.05 -> 1.75 rounds), 93.6 -> 89.9 us/step; 64 x 1e5 on one GPU:
+  // 651 -> 588 us/step (profiles/r02/mattile).
+  if (!env && h->ops->grp && h->esz == 4 && h->R >= 2 && h->r_diag && h->lq_local && h->lj_local &&
+      tile % tile_min == 0) {
+    auto cost = [&](int64_t t) {
+      const int64_t rounds = ((int64_t)h->R * ((h->N + t - 1) / t) + 1023) / 1024;
+      return (double)rounds * ((double)(t / tile_min) + 1.5);
+    };
+    int64_t best = tile;
+    for (int64_t t = tile + tile_min; t <= 8 * tile_min && t <= h->ops->tile_max && t <= h->N; t += tile_min)
+      if (cost(t) < cost(best)) best = t;
+    tile = best;
+  }
   // scalar-state kernels (4-particle chunks, 1024-particle minimum tile) with many
   // replicates: two chunk-loop passes per thread halve the grid and amortise the per-
   // workgroup head load and record reduction (sv64, 64 x 1e6: 463 -> 442 us/step); more
