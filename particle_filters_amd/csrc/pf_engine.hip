@@ -258,8 +258,8 @@ bool choose_geometry(pf_handle* h) {
   // resident on the 256 CUs) over many replicates: the R x G grid runs in rounds of 1024 and a
   // workgroup's time is its chunk passes plus a fixed part (prologue / head, ancestors, record:
   // ~1.5 passes), so take the passes per tile (<= 8) that minimise rounds x (passes + 1.5).
-  // MAT 8 x 1e5: 256 -> 448 (3.05 -> 1.75 rounds), 93.6 -> 89.9 us/step; 64 x 1e5 on one GPU:
-  // 651 -> 588 us/step (profiles/r02/mattile).
+  // MAT 8 x 1e5: 256 -> 448 (3.05 -> 1.75 rounds), 93.6 -> 87.1 us/step; 64 x 1e5 on one GPU:
+  // 651 -> 561 us/step (profiles/r02/mattile).
   if (!env && h->ops->grp && h->esz == 4 && h->R >= 2 && h->r_diag && h->lq_local && h->lj_local &&
       tile % tile_min == 0) {
     auto cost = [&](int64_t t) {
