@@ -159,6 +159,32 @@ pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights);
 pf_status pf_set_state(pf_handle* h, const double* particles, const double* weights);
 int32_t pf_weights_uniform(pf_handle* h);
 
+/* Philox position of the handle (SURVEY.md §5 checkpoint/resume; the reference's counterpart is
+ * the NumPy Generator state behind self.rng, pf.py:100-101).  The next predict draws at `epoch`,
+ * the next update reserves epoch + 1 for its resample; `ep_res` is the epoch of the resample the
+ * last update decided (pending = 1 while it is not yet applied).  pf_set_rng_state moves the
+ * handle to a position (seed = Philox key, replicate_base = counter word of replicate 0);
+ * `pending` is ignored on set. */
+typedef struct pf_rng_state {
+  uint64_t seed;
+  uint32_t epoch;
+  uint32_t ep_res;
+  int32_t replicate_base;
+  int32_t pending;
+} pf_rng_state;
+pf_status pf_get_rng_state(pf_handle* h, pf_rng_state* out);
+pf_status pf_set_rng_state(pf_handle* h, const pf_rng_state* in);
+
+/* Bit-exact checkpoint / resume of the whole filter state at a step boundary (a decided
+ * resample is applied first): particles and UNNORMALISED log-weights in the engine precision,
+ * the tile records, the systematic-CDF prefix, the resident kernel's entry header and the
+ * Philox position.  Restoring into a handle created with the same model and options (shape,
+ * Np, replicates, precision, resample method) continues bitwise as the original would have.
+ * The blob is opaque host memory of pf_checkpoint_bytes(h) bytes. */
+int64_t pf_checkpoint_bytes(pf_handle* h);
+pf_status pf_checkpoint(pf_handle* h, void* buf, int64_t nbytes);
+pf_status pf_restore(pf_handle* h, const void* buf, int64_t nbytes);
+
 /* Weighted mean/cov of the current state, exact two-pass (np.average / np.cov
  * aweights, bias=True; pf.py:266-267), any nx.  mean [R][nx], cov [R][nx][nx]. */
 pf_status pf_moments(pf_handle* h, double* mean, double* cov);

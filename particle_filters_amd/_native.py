@@ -88,6 +88,11 @@ class LedhInfo(C.Structure):
     _fields_ = [("ess", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
 
 
+class RngState(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("epoch", C.c_uint32), ("ep_res", C.c_uint32), ("replicate_base", C.c_int32),
+                ("pending", C.c_int32)]
+
+
 class UpdateInfo(C.Structure):
     _fields_ = [("neff", C.c_double), ("log_norm", C.c_double), ("resample", C.c_int32), ("_pad", C.c_int32)]
 
@@ -114,6 +119,11 @@ SIGNATURES = {
     "pf_set_state": (C.c_int32, [_vp, _dp, _dp]),
     "pf_weights_uniform": (C.c_int32, [_vp]),
     "pf_moments": (C.c_int32, [_vp, _dp, _dp]),
+    "pf_get_rng_state": (C.c_int32, [_vp, C.POINTER(RngState)]),
+    "pf_set_rng_state": (C.c_int32, [_vp, C.POINTER(RngState)]),
+    "pf_checkpoint_bytes": (C.c_int64, [_vp]),
+    "pf_checkpoint": (C.c_int32, [_vp, _vp, C.c_int64]),
+    "pf_restore": (C.c_int32, [_vp, _vp, C.c_int64]),
     "pf_resample_indices": (C.c_int32, [C.c_int32, C.c_int32, _dp, C.c_int64, C.c_double, _dp,
                                         C.POINTER(C.c_int64)]),
     "pf_stream": (_vp, [_vp]),
@@ -221,3 +231,35 @@ def dptr(a):
 
 def device_count() -> int:
     return int(load().pf_device_count())
+
+
+# ---------------------------------------------------------------- Philox position / checkpoints
+def get_rng_state(handle) -> dict:
+    """The handle's Philox position (pf_get_rng_state): seed, epoch, ep_res, replicate_base,
+    pending."""
+    st = RngState()
+    check(load().pf_get_rng_state(handle, C.byref(st)), "pf_get_rng_state")
+    return dict(seed=int(st.seed), epoch=int(st.epoch), ep_res=int(st.ep_res),
+                replicate_base=int(st.replicate_base), pending=bool(st.pending))
+
+
+def set_rng_state(handle, state: dict) -> None:
+    st = RngState(int(state["seed"]), int(state["epoch"]), int(state["ep_res"]), int(state["replicate_base"]), 0)
+    check(load().pf_set_rng_state(handle, C.byref(st)), "pf_set_rng_state")
+
+
+def checkpoint(handle) -> bytes:
+    """Bit-exact snapshot of the filter state (pf_checkpoint): opaque bytes."""
+    lib = load()
+    n = int(lib.pf_checkpoint_bytes(handle))
+    if n <= 0:
+        raise PFError("pf_checkpoint_bytes failed")
+    buf = C.create_string_buffer(n)
+    check(lib.pf_checkpoint(handle, C.cast(buf, C.c_void_p), n), "pf_checkpoint")
+    return buf.raw
+
+
+def restore(handle, blob: bytes) -> None:
+    b = bytes(blob)
+    buf = C.create_string_buffer(b, len(b))
+    check(load().pf_restore(handle, C.cast(buf, C.c_void_p), len(b)), "pf_restore")

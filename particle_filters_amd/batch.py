@@ -125,6 +125,22 @@ class ParticleFilterBatch:
         N.check(N.load().pf_get_weights(self._h, N.dptr(out), None), "pf_get_weights")
         return out
 
+    def rng_state(self) -> dict:
+        """Philox position of the device RNG (epoch of the next predict)."""
+        return N.get_rng_state(self._h)
+
+    def set_rng_state(self, state: dict) -> None:
+        N.set_rng_state(self._h, state)
+
+    def checkpoint(self) -> bytes:
+        """Bit-exact snapshot at the step boundary: particles, unnormalised log-weights, tile
+        records and the Philox position (include/pf_engine.h pf_checkpoint)."""
+        return N.checkpoint(self._h)
+
+    def restore(self, blob: bytes) -> None:
+        """Continue from a :meth:`checkpoint` of a batch with the same model and options."""
+        N.restore(self._h, blob)
+
     @property
     def last_run_resident(self) -> bool:
         """True if the last run() executed as the register-resident whole-run kernel."""

@@ -211,6 +211,8 @@ struct pf_handle {
   // entry header (ResParams::hdr): id of the last resident run whose exit header still
   // describes the state (0: none; any other write of the state clears it), run counter
   unsigned long long res_hdr = 0, res_run = 0;
+  // entry header restored by pf_restore ([R][4] words, id filled in at the next resident run)
+  std::vector<unsigned long long> hdr_restore;
   // bookkeeping before each resident run not yet checked (check_resident), by launch sequence
   // number: an aborted launch (and every later one, which aborts too) is undone to its entry
   struct ResUndo {
@@ -229,6 +231,13 @@ struct pf_handle {
 };
 
 namespace {
+
+// Any write of the state other than a resident run: the last resident exit header (or one a
+// checkpoint restored) no longer describes it.
+void state_written(pf_handle* h) {
+  h->res_hdr = 0;
+  h->hdr_restore.clear();
+}
 
 size_t rec_bytes(const pf_handle* h) { return (size_t)h->R * h->G * h->ops->rec_size * sizeof(double); }
 
@@ -399,7 +408,7 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
     if (st) return st;
     p.head = h->head;
   }
-  if (writes_x || writes_lw || writes_rec) h->res_hdr = 0;  // the resident exit header no longer applies
+  if (writes_x || writes_lw || writes_rec) state_written(h);  // the resident exit header no longer applies
   p.x_in = h->x[h->cx];
   p.x_out = h->x[h->cx ^ 1];
   p.lw_in = h->lw[h->clw];
@@ -558,6 +567,15 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     h->res_seq = 0;
     h->res_hdr = 0;
   }
+  if (!h->hdr_restore.empty()) {  // a restored checkpoint's entry header, under a fresh id
+    const unsigned long long id = ++h->res_run;
+    for (int r = 0; r < h->R; ++r) h->hdr_restore[4 * (size_t)r] = id;
+    HIPCHK(hipMemcpyAsync(h->rsync + hdr_off, h->hdr_restore.data(), h->hdr_restore.size() * sizeof(unsigned long long),
+                          hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));  // pageable source
+    h->res_hdr = id;
+    h->hdr_restore.clear();
+  }
   if (!h->res_unchecked) h->res_undo.clear();
   h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec, h->res_hdr});
   ResParams q;
@@ -616,7 +634,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   q.test_abort = (ta && std::atoi(ta) == 1 && !coop) ? 1 : 0;
   // Resident launches of different handles (streams) on one device never overlap: two grids that
   // each hold part of the CUs would wait for each other's missing workgroups.
-  grid_order_begin(h->device, h->stream);
+  GridOrderScope order(h->device, h->stream);
   if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int r0 = 0; r0 < h->R; r0 += Rg) {
     q.r0 = r0;
@@ -632,7 +650,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
   }
   if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
-  grid_order_end(h->device, h->stream);
+  order.end();
   h->res_hdr = q.hdr_out;  // the state is now what this run's exit header describes
   h->res_tag += (uint32_t)tag_span;
   h->res_flag += (unsigned long long)T + 1;
@@ -690,6 +708,25 @@ pf_status check_resident(pf_handle* h) {
     return fail(PF_E_NAN, "every particle weight is zero or NaN (all-dead filter); call initialize() again");
   return fail(PF_E_HIP, "k_resident: inter-workgroup hand-off timed out (code " + std::to_string(err) +
                             "); call initialize() again");
+}
+
+// Entry of every host API that reads or writes the state: an asynchronous resident run
+// (pf_run_device) not yet checked is waited for and checked first, so nothing acts on a
+// state an aborted launch never produced (PF_E_RETRY then reaches this caller).
+pf_status settle(pf_handle* h) {
+  if (!h->res_unchecked) return PF_OK;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return check_resident(h);
+}
+
+// Every particle weight of some replicate is zero or NaN.  The update that found it has already
+// advanced the state and the Philox epochs, so the handle is poisoned: the next call reports
+// "not initialized" instead of continuing silently from a half-applied step.
+pf_status dead_filter(pf_handle* h, const std::string& where) {
+  h->initialized = false;
+  h->pending = false;
+  return fail(PF_E_NAN, "every particle weight is zero or NaN " + where +
+                            ": the filter is dead; call initialize() again");
 }
 
 }  // namespace
@@ -972,12 +1009,16 @@ pf_status pf_initialize(pf_handle* h, const double* mean, const double* cov, con
   h->initialized = true;
   h->pending = false;
   h->lcum_valid = false;
-  h->res_hdr = 0;
+  state_written(h);
   return PF_OK;
 }
 
 pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
   if (!h) return fail(PF_E_ARG, "null handle");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (!h->chol_q_ok) return fail(PF_E_NOT_PD, "Matrix is not positive definite (Q)");
   if (h->sharded && !replay && h->ops->ch > 1 && h->pbase % 4)
@@ -1015,6 +1056,10 @@ pf_status pf_predict(pf_handle* h, const double* u, const double* replay) {
 
 pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double* mean, double* cov) {
   if (!h || !z) return fail(PF_E_ARG, "null argument");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   HIPCHK(hipSetDevice(h->device));
   if (h->pending) {  // an earlier decision nobody applied: apply it before re-weighting
@@ -1046,8 +1091,7 @@ pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double*
   const int32_t* bf = (const int32_t*)(bl + R);
   for (int r = 0; r < R; ++r)
     if (!(bn[r] > 0.0))  // S == 0 or NaN: no particle has a finite weight
-      return fail(PF_E_NAN, "every particle weight is zero or NaN (replicate " + std::to_string(r) +
-                                "): the filter is dead");
+      return dead_filter(h, "(replicate " + std::to_string(r) + ")");
   bool any = false;
   for (int r = 0; r < R; ++r) {
     if (info) {
@@ -1073,6 +1117,10 @@ pf_status pf_update(pf_handle* h, const double* z, pf_update_info* info, double*
 
 pf_status pf_resample(pf_handle* h, const double* uniforms, const double* jitter, double* mean, double* cov) {
   if (!h) return fail(PF_E_ARG, "null handle");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   if (!h->pending) return PF_OK;
   HIPCHK(hipSetDevice(h->device));
@@ -1246,8 +1294,7 @@ pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int3
   if (neff) std::memcpy(neff, nf.data(), nf.size() * sizeof(double));
   for (size_t i = 0; i < nf.size(); ++i)
     if (!(nf[i] > 0.0))
-      return bail(fail(PF_E_NAN, "every particle weight is zero or NaN at step " + std::to_string(i / R) +
-                                     " (replicate " + std::to_string(i % R) + "): the filter is dead"));
+      return bail(dead_filter(h, "at step " + std::to_string(i / R) + " (replicate " + std::to_string(i % R) + ")"));
   return bail(PF_OK);
 }
 
@@ -1267,6 +1314,10 @@ static pf_status download_real(pf_handle* h, const void* src, size_t n, std::vec
 
 pf_status pf_get_particles(pf_handle* h, double* particles) {
   if (!h || !particles) return fail(PF_E_ARG, "null argument");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   HIPCHK(hipSetDevice(h->device));
   if (h->pending) {
@@ -1304,6 +1355,10 @@ int32_t pf_weights_uniform(pf_handle* h) {
 
 pf_status pf_get_weights(pf_handle* h, double* weights, double* log_weights) {
   if (!h) return fail(PF_E_ARG, "null argument");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   HIPCHK(hipSetDevice(h->device));
   if (h->pending) {
@@ -1438,7 +1493,7 @@ pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, d
   } else if (h->regularize && h->ops->ch > 1 && h->pbase % 4) {
     return fail(PF_E_ARG, "device-RNG jitter of a scalar-state shard needs N_loc % 4 == 0 (or host replay)");
   }
-  h->res_hdr = 0;
+  state_written(h);
   HIPCHK(h->ops->shard_adopt(rows, h->x[h->cx], h->N, h->Npad, h->rec[h->crec], h->G, h->P, h->regularize, rj,
                              h->seed, (uint32_t)h->rep_base, h->ep_res, h->pbase, h->stream, h->nx, h->nz));
   h->pending = false;
@@ -1451,6 +1506,10 @@ pf_status pf_shard_adopt(pf_handle* h, const void* rows, const double* jitter, d
 // diag:61-91 on the device-resident state of every replicate (include/pf_diag.h)
 pf_status pf_state_diagnostics(pf_handle* h, double tol, pf_diagnostics* out) {
   if (!h || !out) return fail(PF_E_ARG, "null argument");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   HIPCHK(hipSetDevice(h->device));
   if (h->pending) {
@@ -1490,6 +1549,10 @@ pf_status pf_state_diagnostics(pf_handle* h, double tol, pf_diagnostics* out) {
 
 pf_status pf_set_state(pf_handle* h, const double* particles, const double* weights) {
   if (!h || !particles) return fail(PF_E_ARG, "null argument");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   HIPCHK(hipSetDevice(h->device));
   const int nx = h->nx, R = h->R;
   std::vector<double> soa((size_t)R * nx * h->Npad, 0.0);
@@ -1499,7 +1562,7 @@ pf_status pf_set_state(pf_handle* h, const double* particles, const double* weig
         soa[((size_t)r * nx + d) * h->Npad + i] = particles[((size_t)r * h->N + i) * nx + d];
   pf_status st = upload_real(h, h->x[h->cx], soa.data(), soa.size());
   if (st) return st;
-  h->res_hdr = 0;
+  state_written(h);
   h->lcum_valid = false;  // uploaded weights: k_cdf materialises their CDF when a resample needs it
   // records: one tile carrying S0 = 1 at m = 0 (so lse = 0), the rest empty; or uniform
   std::vector<double> rec((size_t)R * h->G * h->ops->rec_size, 0.0);
@@ -1535,8 +1598,174 @@ pf_status pf_set_state(pf_handle* h, const double* particles, const double* weig
   return PF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Philox position and bit-exact checkpoint / resume
+// ---------------------------------------------------------------------------
+pf_status pf_get_rng_state(pf_handle* h, pf_rng_state* out) {
+  if (!h || !out) return fail(PF_E_ARG, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  const pf_status s0 = settle(h);
+  if (s0) return s0;
+  out->seed = h->seed;
+  out->epoch = h->epoch;
+  out->ep_res = h->ep_res;
+  out->replicate_base = h->rep_base;
+  out->pending = h->pending ? 1 : 0;
+  return PF_OK;
+}
+
+pf_status pf_set_rng_state(pf_handle* h, const pf_rng_state* in) {
+  if (!h || !in) return fail(PF_E_ARG, "null argument");
+  if (in->epoch == 0) return fail(PF_E_ARG, "epoch 0 is never a handle's position (initialize draws at >= 1)");
+  HIPCHK(hipSetDevice(h->device));
+  const pf_status s0 = settle(h);
+  if (s0) return s0;
+  h->seed = in->seed;
+  h->epoch = in->epoch;
+  h->ep_res = in->ep_res;
+  h->rep_base = in->replicate_base;
+  return PF_OK;
+}
+
+namespace {
+constexpr uint64_t CKPT_MAGIC = 0x3130544b43504650ull;  // "PFPCKT01"
+struct CkptHead {
+  uint64_t magic;
+  int32_t nx, nz, R, G;
+  int64_t N, Npad;
+  int32_t rec_size, esz, method, rep_base;
+  uint64_t seed;
+  uint32_t epoch, ep_res;
+  int32_t lcum_valid, hdr_valid;
+  uint64_t x_bytes, lw_bytes, rec_bytes, lcum_bytes, hdr_bytes;
+};
+CkptHead ckpt_layout(const pf_handle* h) {
+  CkptHead c;
+  std::memset(&c, 0, sizeof(c));
+  c.magic = CKPT_MAGIC;
+  c.nx = h->nx;
+  c.nz = h->nz;
+  c.R = h->R;
+  c.G = h->G;
+  c.N = h->N;
+  c.Npad = h->Npad;
+  c.rec_size = h->ops->rec_size;
+  c.esz = (int32_t)h->esz;
+  c.method = h->method;
+  c.x_bytes = (uint64_t)h->R * h->nx * h->Npad * h->esz;
+  c.lw_bytes = (uint64_t)h->R * h->Npad * h->esz;
+  c.rec_bytes = rec_bytes(h);
+  c.lcum_bytes = h->lcum[0] ? (uint64_t)h->R * h->N * sizeof(double) : 0;
+  c.hdr_bytes = 4 * (uint64_t)h->R * sizeof(unsigned long long);
+  return c;
+}
+uint64_t ckpt_total(const CkptHead& c) {
+  return sizeof(CkptHead) + c.x_bytes + c.lw_bytes + c.rec_bytes + c.lcum_bytes + c.hdr_bytes;
+}
+size_t res_hdr_offset(const pf_handle* h) {  // entry headers inside rsync (run_resident's layout)
+  return RCOPIES * gran_copy_stride(h->R) + 2 * (size_t)h->R * RMAXG + 4;
+}
+}  // namespace
+
+int64_t pf_checkpoint_bytes(pf_handle* h) {
+  if (!h) return -1;
+  return (int64_t)ckpt_total(ckpt_layout(h));
+}
+
+pf_status pf_checkpoint(pf_handle* h, void* buf, int64_t nbytes) {
+  if (!h || !buf) return fail(PF_E_ARG, "null argument");
+  if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
+  HIPCHK(hipSetDevice(h->device));
+  pf_status st = settle(h);
+  if (st) return st;
+  if (h->pending) {  // the checkpoint is a step boundary: a decided resample is applied first
+    st = apply_pending(h, nullptr, nullptr, false);
+    if (st) return st;
+  }
+  CkptHead c = ckpt_layout(h);
+  if (nbytes < (int64_t)ckpt_total(c)) return fail(PF_E_ARG, "checkpoint buffer too small (pf_checkpoint_bytes)");
+  c.seed = h->seed;
+  c.epoch = h->epoch;
+  c.ep_res = h->ep_res;
+  c.rep_base = h->rep_base;
+  c.lcum_valid = (c.lcum_bytes && h->lcum_valid) ? 1 : 0;
+  char* o = (char*)buf + sizeof(CkptHead);
+  HIPCHK(hipMemcpyAsync(o, h->x[h->cx], c.x_bytes, hipMemcpyDeviceToHost, h->stream));
+  o += c.x_bytes;
+  HIPCHK(hipMemcpyAsync(o, h->lw[h->clw], c.lw_bytes, hipMemcpyDeviceToHost, h->stream));
+  o += c.lw_bytes;
+  HIPCHK(hipMemcpyAsync(o, h->rec[h->crec], c.rec_bytes, hipMemcpyDeviceToHost, h->stream));
+  o += c.rec_bytes;
+  if (c.lcum_bytes) {
+    if (c.lcum_valid) HIPCHK(hipMemcpyAsync(o, h->lcum[h->clcum], c.lcum_bytes, hipMemcpyDeviceToHost, h->stream));
+    else std::memset(o, 0, c.lcum_bytes);
+    o += c.lcum_bytes;
+  }
+  // the resident exit header that describes this state (a run that follows takes it instead of
+  // reducing the records: part of the state for a bit-exact continuation)
+  std::memset(o, 0, c.hdr_bytes);
+  if (!h->hdr_restore.empty()) {
+    std::memcpy(o, h->hdr_restore.data(), c.hdr_bytes);
+    c.hdr_valid = 1;
+  } else if (h->res_hdr && h->rsync) {
+    HIPCHK(hipMemcpyAsync(o, h->rsync + res_hdr_offset(h), c.hdr_bytes, hipMemcpyDeviceToHost, h->stream));
+    c.hdr_valid = 1;
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  std::memcpy(buf, &c, sizeof(c));
+  return PF_OK;
+}
+
+pf_status pf_restore(pf_handle* h, const void* buf, int64_t nbytes) {
+  if (!h || !buf) return fail(PF_E_ARG, "null argument");
+  if (nbytes < (int64_t)sizeof(CkptHead)) return fail(PF_E_ARG, "checkpoint too short");
+  CkptHead c;
+  std::memcpy(&c, buf, sizeof(c));
+  const CkptHead want = ckpt_layout(h);
+  if (c.magic != CKPT_MAGIC) return fail(PF_E_ARG, "not a pf_checkpoint blob");
+  if (c.nx != want.nx || c.nz != want.nz || c.R != want.R || c.G != want.G || c.N != want.N || c.Npad != want.Npad ||
+      c.rec_size != want.rec_size || c.esz != want.esz || c.method != want.method || c.x_bytes != want.x_bytes ||
+      c.lw_bytes != want.lw_bytes || c.rec_bytes != want.rec_bytes || c.lcum_bytes != want.lcum_bytes ||
+      c.hdr_bytes != want.hdr_bytes)
+    return fail(PF_E_ARG, "checkpoint of a different filter configuration (shape, N, replicates, precision or method)");
+  if (nbytes < (int64_t)ckpt_total(c)) return fail(PF_E_ARG, "checkpoint truncated");
+  HIPCHK(hipSetDevice(h->device));
+  pf_status st = settle(h);
+  if (st && st != PF_E_NAN) return st;  // a dead state is being replaced: fine
+  const char* o = (const char*)buf + sizeof(CkptHead);
+  HIPCHK(hipMemcpyAsync(h->x[h->cx], o, c.x_bytes, hipMemcpyHostToDevice, h->stream));
+  o += c.x_bytes;
+  HIPCHK(hipMemcpyAsync(h->lw[h->clw], o, c.lw_bytes, hipMemcpyHostToDevice, h->stream));
+  o += c.lw_bytes;
+  HIPCHK(hipMemcpyAsync(h->rec[h->crec], o, c.rec_bytes, hipMemcpyHostToDevice, h->stream));
+  o += c.rec_bytes;
+  if (c.lcum_bytes) {
+    if (c.lcum_valid) HIPCHK(hipMemcpyAsync(h->lcum[h->clcum], o, c.lcum_bytes, hipMemcpyHostToDevice, h->stream));
+    o += c.lcum_bytes;
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  state_written(h);
+  if (c.hdr_valid) {
+    h->hdr_restore.assign((const unsigned long long*)o, (const unsigned long long*)o + 4 * (size_t)h->R);
+  }
+  h->lcum_valid = c.lcum_valid != 0;
+  h->seed = c.seed;
+  h->epoch = c.epoch;
+  h->ep_res = c.ep_res;
+  h->rep_base = c.rep_base;
+  h->pending = false;
+  h->head_valid = false;
+  h->shard_cdf_ep = 0;
+  h->initialized = true;
+  return PF_OK;
+}
+
 pf_status pf_moments(pf_handle* h, double* mean, double* cov) {
   if (!h) return fail(PF_E_ARG, "null handle");
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
   if (!h->initialized) return fail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
   HIPCHK(hipSetDevice(h->device));
   if (h->pending) {

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <optional>
 #include <vector>
 
 #include "../../include/pf_ledh.h"
@@ -256,8 +257,7 @@ static bool is_diag(const double* A, int n) {
 }  // namespace pf
 
 using namespace pf::ledh;
-using pf::grid_order_begin;
-using pf::grid_order_end;
+using pf::GridOrderScope;
 using pf::grid_order_forget;
 
 struct pf_ledh_handle {
@@ -877,7 +877,8 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
           st = lfail(PF_E_HIP, "run: batched flow-table launch failed");
     }
     const bool fused_run = h->fused_nbk > 0 && dTab;
-    if (fused_run) grid_order_begin(h->device, h->stream);  // no overlap with another handle's grid
+    std::optional<GridOrderScope> order;  // no overlap with another handle's grid
+    if (fused_run) order.emplace(h->device, h->stream);
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
       if (ekf && t % CH == 0 && hipStreamWaitEvent(h->stream, evs[1 + t / CH], 0) != hipSuccess) {
         st = lfail(PF_E_HIP, "run: stream wait failed");
@@ -920,7 +921,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
                         df + t, dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
     }
-    if (fused_run) grid_order_end(h->device, h->stream);
+    if (order) order->end();
     if (ekf) (void)hipStreamSynchronize(h->side);
     for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     if (st != PF_OK) break;

@@ -28,22 +28,35 @@ inline bool grid_order_off() {  // PF_NO_ORDER=1: diagnostics only (unsafe with 
   }();
   return off;
 }
-inline void grid_order_begin(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64 || grid_order_off()) return;
-  GridOrder& o = grid_order();
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
-}
-inline void grid_order_end(int dev, hipStream_t s) {
-  if (dev < 0 || dev >= 64 || grid_order_off()) return;
-  GridOrder& o = grid_order();
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (!o.ev[dev] && hipEventCreateWithFlags(&o.ev[dev], hipEventDisableTiming) != hipSuccess) {
-    o.ev[dev] = nullptr;
-    return;
+// Scope of one or more grid-synchronising launches on stream s: the process-wide lock is held
+// from before the wait on the previous grid's event until this grid's event is recorded, so two
+// host threads driving different handles cannot both pass the wait before either records
+// (their grids would then be issued unordered).  Construct right before the launches; the
+// event is recorded by end() or, on an early return, by the destructor.
+class GridOrderScope {
+ public:
+  GridOrderScope(int dev, hipStream_t s) : dev_(dev), s_(s) {
+    if (dev < 0 || dev >= 64 || grid_order_off()) return;
+    lk_ = std::unique_lock<std::mutex>(grid_order().mu);
+    GridOrder& o = grid_order();
+    if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
   }
-  if (hipEventRecord(o.ev[dev], s) == hipSuccess) o.last[dev] = s;
-}
+  void end() {
+    if (!lk_.owns_lock()) return;
+    GridOrder& o = grid_order();
+    if (!o.ev[dev_] && hipEventCreateWithFlags(&o.ev[dev_], hipEventDisableTiming) != hipSuccess) o.ev[dev_] = nullptr;
+    if (o.ev[dev_] && hipEventRecord(o.ev[dev_], s_) == hipSuccess) o.last[dev_] = s_;
+    lk_.unlock();
+  }
+  ~GridOrderScope() { end(); }
+  GridOrderScope(const GridOrderScope&) = delete;
+  GridOrderScope& operator=(const GridOrderScope&) = delete;
+
+ private:
+  int dev_;
+  hipStream_t s_;
+  std::unique_lock<std::mutex> lk_;
+};
 // a stream about to be destroyed is no longer "the last one" (the event stays valid)
 inline void grid_order_forget(int dev, hipStream_t s) {
   if (dev < 0 || dev >= 64) return;

@@ -605,6 +605,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   constexpr bool outwg = decltype(out_tag)::value;  // b == G - 1
   // ---- entry state (k_step layout) and its normaliser ------------------------
   float x[RPPT], l[RPPT];
+  double F0 = 0.0, T0 = 0.0;  // entry frame and absolute log mass (from the entry header)
   {
     // the particles' loads first: their latency overlaps the records' reduction below
     float lr[RPPT];
@@ -631,8 +632,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (p.hdr_in) {
       typedef const __attribute__((address_space(4))) unsigned long long cu64;
       const cu64* hp = (const cu64*)(p.hdr + (size_t)r * 4);
-      if (hp[0] == p.hdr_in) {
-        lse0d = __longlong_as_double((long long)hp[1]);
+      if (hp[0] == p.hdr_in) {  // the exit frame continues: raw log-weights, its F and absolute mass
+        T0 = __longlong_as_double((long long)hp[1]);
+        F0 = __longlong_as_double((long long)hp[3]);
         uniform0 = hp[2] != 0ull;
         have_hdr = true;
       }
@@ -648,7 +650,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     if (b == 0 && r == 0 && t == 0) g_pf_stamps[20] = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
-    for (int e = 0; e < RPPT; ++e) l[e] = (i0 + e >= N) ? -INFINITY : (uniform0 ? lunif : lr[e] - lse0);
+    for (int e = 0; e < RPPT; ++e)
+      l[e] = (i0 + e >= N) ? -INFINITY : (uniform0 ? lunif : (have_hdr ? lr[e] : lr[e] - lse0));
+    if (uniform0) F0 = T0 = 0.0;
   }
   if (t == 0) arr_sh = arr_old - p.arrive0 < RABORT;  // arrived after an abort: leave
   __syncthreads();
@@ -667,8 +671,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   unsigned vnext = 0;      // next sequence number to verify
   unsigned nres = 0;       // hand-offs so far (flag tags)
   unsigned it = 0;         // iteration parity (LDS double buffers)
-  double F = 0.0;          // frame of the live log-weights
-  double Tprev = 0.0;      // absolute log mass of the last verified step
+  // frame of the live log-weights (the log-weights are l + F); absolute log mass of the last
+  // verified step.  A run that follows a resident run continues that run's frame (entry header):
+  // the raw exit log-weights with its F and mass, so a run cut into pieces is bitwise the
+  // uninterrupted run
+  double F = F0;
+  double Tprev = T0;
   bool prev_res = false;   // last verified step resampled: next record carries its aux sums
   bool have_aux = false;   // the live state was just gathered
   bool rec_aux = false;    // the record being published carries the aux sums
@@ -676,9 +684,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool last_uniform = false;
   bool alive = true;
   bool aborted = false;
-  double Tlast = 0.0;   // absolute log mass of the last verified (not resampled) step
+  double Tlast = T0;    // absolute log mass of the last verified (not resampled) step
   int last_cur = 0;     // mslot buffer of the last computed step, and its frame
-  double F_last = 0.0;
+  double F_last = F0;
   float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
   int64_t zbase = -64;
   while (alive) {
@@ -1027,6 +1035,30 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       __syncthreads();
       all = quad_all(cur);
     }
+    if (alive && !verified_any && gridDim.y > 1) {
+      // A verified step proves only that THIS replicate's workgroups arrived.  Several replicates
+      // in one plain launch: before anything is written in place, wait until the whole grid has
+      // counted in - or the launch aborts (another replicate's workgroup found it incomplete):
+      // then every replicate leaves with its state untouched.
+      if (t == 0) {
+        int res = 0;
+        while (res == 0) {
+          const unsigned long long rel = ld_sc1(p.arrive) - p.arrive0;
+          if (rel >= RABORT) res = 2;
+          else if (rel >= total_wg) res = 1;
+          else if (__builtin_amdgcn_s_memrealtime() - t_start > RARRIVE_TICKS)
+            res = res_try_abort(p.arrive, p.err, p.arrive0, total_wg, p.seq) ? 2 : 1;
+          else
+            __builtin_amdgcn_s_sleep(2);
+        }
+        arr_sh = res;
+      }
+      __syncthreads();
+      if (arr_sh == 2) {
+        aborted = true;
+        alive = false;
+      }
+    }
     if (!alive) break;
     verified_any = true;
     PF_RMARK(12);  // slow polls
@@ -1266,12 +1298,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
     }
   }
-  // entry header of the next launch: log sum of the exit log-weights = Tlast - F (the last
-  // verified step's mass in the exit frame: the fp32 residual of the final shift), or uniform
+  // entry header of the next launch: the exit frame F and the last verified step's absolute log
+  // mass Tlast (the exit log-weights sum to e^(Tlast - F): the fp32 residual of the final shift),
+  // or uniform
   if (b == 0 && t == 0 && alive) {
     unsigned long long* hp = p.hdr + (size_t)r * 4;
-    hp[1] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : Tlast - F);
+    hp[1] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : Tlast);
     hp[2] = last_uniform ? 1ull : 0ull;
+    hp[3] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : F);
     hp[0] = p.hdr_out;
   }
 #ifdef PF_STAMPS

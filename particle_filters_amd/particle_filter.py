@@ -331,6 +331,36 @@ class ParticleFilter:
             self.state.cov = c
         return res
 
+    # ------------------------------------------------------ checkpoint / resume
+    def rng_state(self) -> dict:
+        """Philox position of the device RNG (epoch of the next predict)."""
+        return N.get_rng_state(self._handle)
+
+    def set_rng_state(self, state: dict) -> None:
+        N.set_rng_state(self._handle, state)
+
+    def checkpoint(self) -> dict:
+        """Bit-exact snapshot at the step boundary: the engine blob (particles, unnormalised
+        log-weights, tile records, Philox position) plus the host side (step count, ESS, the
+        host Generator's state for rng_mode='host')."""
+        assert self.state is not None, "Filter not initialized."
+        blob = N.checkpoint(self._handle)
+        return dict(engine=blob, t=int(self.state.t), ess=float(self._ess),
+                    rng=self.rng.bit_generator.state if hasattr(self.rng, "bit_generator") else None)
+
+    def restore(self, ckpt: dict) -> PFState:
+        """Continue from :meth:`checkpoint` of a filter with the same model and options."""
+        N.restore(self._handle, ckpt["engine"])
+        if ckpt.get("rng") is not None and hasattr(self.rng, "bit_generator"):
+            self.rng.bit_generator.state = ckpt["rng"]
+        self._version += 1
+        self._ess = float(ckpt["ess"])
+        mean = np.empty(self.nx)
+        cov = np.empty((self.nx, self.nx))
+        N.check(N.load().pf_moments(self._handle, N.dptr(mean), N.dptr(cov)), "pf_moments")
+        self.state = _DeviceState(self, mean, cov, int(ckpt["t"]))
+        return self.state
+
     # ------------------------------------------------- reference private helpers
     def _systematic_resample(self, weights: Array) -> Array:
         """Ancestor indices of systematic resampling (pf.py:146-171), computed on the GPU

@@ -249,6 +249,11 @@ class ShardedParticleFilter:
         if rng_mode not in ("device", "host"):
             raise ValueError("rng_mode must be 'device' or 'host'")
         self.rng_mode = rng_mode
+        if rng_mode == "host" and comm is not None and rng is None:
+            # every rank replays the SAME reference draw stream (U, normals of all Np rows) and
+            # takes its own rows: an unseeded Generator per rank would give the ranks different
+            # systematic U / slot ranges and mismatched exchanges
+            raise ValueError("rng_mode='host' across ranks needs rng: a Generator seeded identically on every rank")
         self.rng = np.random.default_rng() if rng is None else rng
         if self.Np % self.W:
             raise ValueError("Np must be W * N_loc")

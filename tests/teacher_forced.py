@@ -1,0 +1,170 @@
+"""State-teacher-forced one-step parity of the benchmarked fp32 kernels (helper of the -m gpu tests).
+
+At a step boundary t of a benchmarked run the engine's own fp32 state S_t (particles, normalised
+log-weights, Philox position: ``ParticleFilterBatch.checkpoint`` / ``rng_state``) is loaded into
+the fp64 oracle (``oracle.sir_philox.PhiloxSIROracle`` = ``oracle.pf_oracle.SIROracle``, pinned bit
+for bit to the reference's outputs, on the engine's Philox draws) and both run ONE step
+(pf.py:223-269 + _resample pf.py:188-220) with identical draws.  The comparison is split so each
+part has a sharp tolerance:
+
+1. the pre-resample step.  The engine's predicted particles and weights come from a twin handle
+   with resample_thresh = 0 into which the same checkpoint is restored (the same kernel, the same
+   arithmetic; only the decision differs): particles within fp32 rounding, the weights' total
+   variation distance, Neff (rel), the decision (it may differ only where Neff is within 1e-3 N of
+   the threshold);
+2. the engine's resampling on its own weights: the post-step particles are EXACTLY
+   ``x'_e[searchsorted(cumsum(w_e), (U + i)/N, 'right')]`` (+ the jitter), U the step's Philox
+   uniform - bit-exact indices, except where a position lies within 1e-12 of the engine's CDF
+   (fp64 summation order);
+3. the engine's ancestors against the oracle's: they differ only at near-ties, i.e. slots whose
+   position lies within the CDF difference that part 1 measured (|pos - cdf_o| <= max|cdf_e - cdf_o|),
+   and the posterior mean equals the oracle's with the engine's ancestors within 1e-5 x scale.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import sir_philox as SP
+from oracle.pf_oracle import OracleState, systematic_indices
+
+
+class StepOracle(SP.PhiloxSIROracle):
+    """PhiloxSIROracle that keeps the pre-resample particles / weights and the systematic U."""
+
+    def _resample(self, particles, weights):
+        self.pre_x = np.array(particles, float)
+        self.pre_w = np.array(weights, float)
+        self.U = None
+        self.idx = None
+        return super()._resample(particles, weights)
+
+    def _systematic_resample(self, weights):
+        self.U = float(self.rng.random())
+        self.idx = systematic_indices(weights, self.U)
+        return self.idx
+
+
+def margins(w, U, idx):
+    """|position - nearest edge of the chosen ancestor's CDF interval| per slot (fp64 cumsum)."""
+    N = len(w)
+    cdf = np.cumsum(w)
+    cdf[-1] = 1.0
+    pos = (U + np.arange(N)) / N
+    lo = np.where(idx > 0, cdf[np.maximum(idx - 1, 0)], 0.0)
+    return np.minimum(pos - lo, cdf[idx] - pos), cdf, pos
+
+
+def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_pre, we_pre, neff_e, neff_e0,
+             flag_e, mean_e, xe_post, scale, bm24=True, tie_floor=1e-7, exp_err=2.0 ** -22, K=8):
+    """Compare one engine step with the oracle's from the same state.  Returns a dict of measured
+    quantities (see module docstring); tolerances are applied by ``check``."""
+    N, nx = x0.shape
+    o = StepOracle(ssm.g_vec, ssm.h_vec, Q, R, seed=seed, rep=rep, bm24=bm24, epoch=epoch, Np=N,
+                   resample_thresh=thresh, resample_method=method, regularize_after_resample=reg, vectorized=True)
+    o.state = OracleState(np.array(x0, float), np.array(w0, float), np.zeros(nx), np.eye(nx), 0)
+    st = o.step(np.atleast_1d(np.asarray(z, float)))
+    out = dict(N=N)
+    # 1. pre-resample: particles, weights, Neff, decision
+    out["dx_pre"] = float(np.max(np.abs(xe_pre - o.pre_x)))
+    out["tv_w"] = float(0.5 * np.sum(np.abs(we_pre - o.pre_w)))
+    cdf_o = np.cumsum(o.pre_w)
+    cdf_e = np.cumsum(we_pre)
+    out["dcdf"] = float(np.max(np.abs(cdf_e - cdf_o)))
+    out["neff_rel"] = float(abs(neff_e / o.last_neff - 1.0))
+    out["neff_twin_equal"] = bool(neff_e == neff_e0)
+    out["flag_e"], out["flag_o"] = bool(flag_e), bool(o.last_resampled)
+    out["near_threshold"] = bool(abs(o.last_neff - thresh * N) / N < 1e-3)
+    out["resampled"] = bool(flag_e)
+    if not flag_e:
+        out["dx_post"] = float(np.max(np.abs(xe_post - xe_pre)))  # no resample: the state is x'_e itself
+        mo = st.mean if not o.last_resampled else np.average(o.pre_x, axis=0, weights=o.pre_w)
+        out["dmean"] = float(np.max(np.abs(mean_e - mo)))
+        out["dmean_oracle"] = out["dmean"]
+        out["n_anc_self_mismatch"] = out["n_anc_diff"] = 0
+        out["max_margin_diff"] = 0.0
+        return out
+    assert method == "systematic"
+    # the step's systematic U and jitter normals (the oracle's own draws, whatever it decided)
+    U = float(SP.philox.uniform53(seed, 0, rep, epoch + 1))
+    jit = np.zeros_like(xe_post)
+    if reg:  # 0.001 chol(Q) n on the resample epoch's jitter stream (pf.py:212-218)
+        try:
+            Lq = np.linalg.cholesky(Q)
+        except np.linalg.LinAlgError:
+            Lq = np.linalg.cholesky(Q + 1e-12 * np.eye(nx))
+        jit = o.prng.at(epoch + 1, SP.philox.STREAM_JITTER).standard_normal((N, nx)) @ (0.001 * Lq.T)
+    # 2. the engine's ancestors, read off its post-step particles: slot i holds x'_e[j] (+ the slot's
+    #    jitter) for one j; candidates are the oracle's ancestor and its index neighbours
+    idx_o = systematic_indices(o.pre_w, U)
+    if o.idx is not None:
+        assert np.array_equal(idx_o, o.idx)
+    cdf_o = np.cumsum(o.pre_w)
+    cdf_o[-1] = 1.0
+    pos = (U + np.arange(N)) / N
+    band = max(tie_floor, out["dcdf"]) + exp_err  # the engine's CDF may sit this far from the oracle's
+
+    def dist(j):  # distance of pos to the oracle's CDF interval of ancestor j
+        lo = np.where(j > 0, cdf_o[np.maximum(j - 1, 0)], 0.0)
+        return np.maximum(0.0, np.maximum(lo - pos, pos - cdf_o[j]))
+
+    tol_copy = 0.0 if not reg else 4e-7 * scale  # a copy is exact (the jitter: fp32 vs fp64 add)
+    idx_e = np.full(N, -1, dtype=np.int64)
+    for k in sorted(range(-K, K + 1), key=abs):
+        cand = np.clip(idx_o + k, 0, N - 1)
+        todo = idx_e < 0
+        if not todo.any():
+            break
+        hit = np.max(np.abs(xe_post[todo] - (xe_pre[cand[todo]] + jit[todo])), axis=1) <= tol_copy
+        sel = np.nonzero(todo)[0][hit]
+        idx_e[sel] = cand[sel]
+    # a near-tie may also skip particles of (numerically) zero weight, far away in index: the few
+    # slots not matched near the oracle's ancestor are looked up among all predicted particles
+    rest = np.nonzero(idx_e < 0)[0]
+    if 0 < rest.size <= 256:
+        for i in rest:
+            m = np.nonzero(np.max(np.abs(xe_pre + jit[i] - xe_post[i]), axis=1) <= tol_copy)[0]
+            if m.size:  # the copy whose oracle CDF interval is nearest the slot's position
+                lo = np.where(m > 0, cdf_o[np.maximum(m - 1, 0)], 0.0)
+                dm = np.maximum(0.0, np.maximum(lo - pos[i], pos[i] - cdf_o[m]))
+                idx_e[i] = m[np.argmin(dm)]
+    out["n_unmatched"] = int(np.sum(idx_e < 0))
+    diff = (idx_e >= 0) & (idx_e != idx_o)
+    d = dist(np.maximum(idx_e, 0))
+    out["n_anc_diff"] = int(np.sum(diff))
+    out["max_margin_diff"] = float(np.max(d[diff])) if diff.any() else 0.0
+    out["band"] = band
+    idx_e = np.where(idx_e >= 0, idx_e, idx_o)
+    forced = o.pre_x[idx_e] + jit
+    out["dmean"] = float(np.max(np.abs(mean_e - forced.mean(axis=0))))
+    out["dmean_oracle"] = float(np.max(np.abs(mean_e - st.mean)))
+    out["dx_post"] = float(np.max(np.abs(xe_post - forced)))
+    out["n_anc_self_mismatch"] = out["n_unmatched"]
+    return out
+
+
+def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5):
+    """Tolerances (stated in the test module): particles tol_x x scale (fp32 rounding of one step),
+    weights' TV distance tol_tv, Neff rel tol_neff, decisions identical unless Neff is within
+    1e-3 N of the threshold; every post-step slot is a copy of one of the engine's predicted
+    particles whose oracle CDF interval lies within the band of the position (band = max(tie
+    floor, measured max|cdf_e - cdf_o|) + the engine's fp32-exponential error); the posterior mean
+    within tol_mean x scale of the oracle's particles under the engine's ancestors."""
+    assert c["neff_twin_equal"], "the twin (thresh 0) step must have the same Neff bit for bit"
+    assert c["dx_pre"] <= tol_x * scale, c
+    assert c["tv_w"] <= tol_tv, c
+    assert c["neff_rel"] <= tol_neff, c
+    if c["flag_e"] != c["flag_o"]:
+        assert c["near_threshold"], c
+    assert c["n_anc_self_mismatch"] == 0, c
+    if c["resampled"]:
+        assert c["max_margin_diff"] <= c["band"], c
+    assert c["dmean"] <= tol_mean * scale, c
+    assert c["dx_post"] <= 2 * tol_x * scale, c
+
+
+def fmt(t, c):
+    return (f"t={t:4d} res={int(c['flag_e'])}/{int(c['flag_o'])} dx_pre={c['dx_pre']:.2e} tvw={c['tv_w']:.2e} "
+            f"dcdf={c['dcdf']:.2e} dNeff={c['neff_rel']:.2e} dmean={c['dmean']:.2e} (vs oracle's own "
+            f"ancestors {c['dmean_oracle']:.2e}) anc_diff={c['n_anc_diff']} max_margin={c['max_margin_diff']:.2e} "
+            f"band={c.get('band', 0.0):.2e} unmatched={c['n_anc_self_mismatch']}")

@@ -178,3 +178,14 @@ def test_ledh_model_registry_and_validation():
     d2, keep2 = M.describe(M.LinearTransition(np.eye(5)), M.LinearObservation(np.ones((1, 5))), np.eye(5), np.eye(1))
     opts = NV.LedhOpts(10, 8, 0.5, 1, 0, 0)
     assert lib.pf_ledh_create(C.byref(d2), C.byref(opts), C.byref(h_)) == NV.PF_E_UNSUPPORTED
+
+
+def test_checkpoint_api_validates_arguments_without_a_device():
+    lib = NV.load()
+    st = NV.RngState()
+    assert lib.pf_get_rng_state(None, C.byref(st)) == NV.PF_E_ARG
+    assert lib.pf_set_rng_state(None, C.byref(st)) == NV.PF_E_ARG
+    assert lib.pf_checkpoint_bytes(None) == -1
+    buf = C.create_string_buffer(256)
+    assert lib.pf_checkpoint(None, C.cast(buf, C.c_void_p), 256) == NV.PF_E_ARG
+    assert lib.pf_restore(None, C.cast(buf, C.c_void_p), 256) == NV.PF_E_ARG

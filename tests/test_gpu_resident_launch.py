@@ -80,6 +80,30 @@ def test_host_run_repeats_an_aborted_launch(data, monkeypatch):
     same(ref, got)
 
 
+def test_abort_with_two_replicates_repeats_bitwise(data, monkeypatch):
+    """Two replicates in one plain launch (advisor finding): a verified step of one replicate does
+    not prove that the other replicate's workgroups arrived, so nothing is written in place until
+    the whole grid has counted in.  Forced abort (the last workgroup of replicate 0 arrives late):
+    pf_run repeats the run cooperatively, bitwise equal to an undisturbed run."""
+    x0, Z = data
+
+    def run():
+        pf = ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]],
+                                 Np=N, n_replicates=2, seed=42)
+        pf.initialize([x0], [[0.5]])
+        r = pf.run(Z)
+        assert pf.last_run_resident
+        pf.close()
+        return r
+
+    monkeypatch.delenv("PF_TEST_ABORT", raising=False)
+    ref = run()
+    monkeypatch.setenv("PF_TEST_ABORT", "1")
+    got = run()
+    same(ref, got)
+    assert not np.array_equal(ref.means[:, 0], ref.means[:, 1])
+
+
 class DeviceRun:
     """pf_run_device on torch buffers (async), outputs fetched after pf_synchronize."""
 

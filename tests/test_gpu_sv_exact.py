@@ -101,9 +101,9 @@ def test_all_dead_step_raises(path, golden_sv, monkeypatch):
     b.initialize([0.0], [[0.5]])
     with pytest.raises(FloatingPointError):
         b.run(Y[:, None])
-    if path == "resident":  # the in-place state is gone: the handle must be re-initialised
-        with pytest.raises(AssertionError, match="Filter not initialized"):
-            b.run(Y[:5, None])
+    # the state has moved past the dead step on either path: the handle is poisoned until re-initialised
+    with pytest.raises(AssertionError, match="Filter not initialized"):
+        b.run(Y[:5, None])
     b.initialize([0.0], [[0.5]])
     r = b.run(Y[:10, None])
     assert np.all(np.isfinite(r.means))
@@ -117,3 +117,26 @@ def test_all_dead_update_api_raises(golden_sv):
     pf.step(np.array([0.4]))
     with pytest.raises(FloatingPointError):
         pf.step(np.array([np.nan]))
+    with pytest.raises(AssertionError, match="Filter not initialized"):
+        pf.step(np.array([0.4]))
+
+
+@pytest.mark.parametrize("path", ["resident", "step"])
+def test_one_dead_replicate_poisons_the_batch(path, golden_sv, monkeypatch):
+    """R = 2, only replicate 1 sees the NaN observation: the batch reports FloatingPointError and
+    refuses to continue (the live replicate's step has advanced with the dead one's)."""
+    if path == "step":
+        monkeypatch.setenv("PF_RESIDENT", "0")
+    Y = golden_sv["Y0"][1:30].copy()
+    Zr = np.stack([Y, Y], axis=1)[:, :, None]
+    Zr[11, 1, 0] = np.nan
+    b = ParticleFilterBatch(M.SVTransition(0.95), M.SVExactObservation(1.0), [[0.04]], None, Np=20_000, n_replicates=2,
+                            seed=4)
+    b.initialize([0.0], [[0.5]])
+    with pytest.raises(FloatingPointError):
+        b.run(Zr)
+    with pytest.raises(AssertionError, match="Filter not initialized"):
+        b.run(Zr[:3])
+    b.initialize([0.0], [[0.5]])
+    assert np.all(np.isfinite(b.run(Zr[:10]).means))
+    b.close()

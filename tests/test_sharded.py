@@ -176,3 +176,15 @@ def test_host_replay_shards_match_reference(name, W, golden_runs, golden_sv, gol
     np.testing.assert_allclose(neff, ref["neff"], rtol=1e-9)
     parts = np.concatenate([pf.local_particles()[s] for s in range(W)])
     np.testing.assert_allclose(parts, ref["final_particles"], rtol=1e-9, atol=1e-9)
+
+
+def test_host_replay_across_ranks_needs_a_shared_generator():
+    """rng_mode='host' with a communicator: every rank must replay the same draw stream, so an
+    implicit unseeded Generator per rank is refused (advisor finding)."""
+    class _Comm:
+        world, rank = 2, 0
+
+    ssm = ssm_oracle.sv_logsq(0.95, 0.2, 1.0)
+    with pytest.raises(ValueError, match="seeded identically"):
+        SH.ShardedParticleFilter(M.SVTransition(0.95), M.SVLogSqObservation(1.0), ssm.Q, ssm.R, Np=2000,
+                                 comm=_Comm(), rng_mode="host")
