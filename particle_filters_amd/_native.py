@@ -183,6 +183,8 @@ def load() -> C.CDLL:
                 "(python -c 'import __graft_entry__ as g; g.build()' or make -C particle_filters_amd/csrc)")
         lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
+            if "PF_LIB" in os.environ and not hasattr(lib, name):
+                continue  # an experiment variant built from an older tree (tools/gpu_ab.sh)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

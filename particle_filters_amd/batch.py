@@ -29,7 +29,7 @@ from . import models as M
 @dataclass
 class RunResult:
     means: np.ndarray      # [T][R][nx]
-    covs: Optional[np.ndarray]  # [T][R][nx][nx] (nx <= 4) else None
+    covs: Optional[np.ndarray]  # [T][R][nx][nx] (None when run(with_cov=False))
     neff: np.ndarray       # [T][R] pre-resample 1/sum w^2
     flags: np.ndarray      # [T][R] bool, resampled at that step
     log_norm: np.ndarray   # [T][R]
@@ -92,8 +92,10 @@ class ParticleFilterBatch:
         rn = None if replay_normals is None else np.ascontiguousarray(replay_normals, dtype=float)
         N.check(N.load().pf_initialize(self._h, N.dptr(m), N.dptr(c), N.dptr(rn)), "pf_initialize")
 
-    def run(self, Z, U=None, *, first_update_only: bool = False) -> RunResult:
-        """Filter observations Z ([T][nz], shared by all replicates, or [T][R][nz])."""
+    def run(self, Z, U=None, *, first_update_only: bool = False, with_cov: bool = True) -> RunResult:
+        """Filter observations Z ([T][nz], shared by all replicates, or [T][R][nz]).  Every step's
+        posterior covariance (pf.py:266-267) is computed on the device for any nx; with_cov=False
+        skips it (nx > 4: one MFMA covariance launch pair per step)."""
         Z = np.asarray(Z, float)
         T = Z.shape[0]
         Zr = np.ascontiguousarray(np.broadcast_to(Z.reshape(T, -1, self.nz), (T, self.n_replicates, self.nz)))
@@ -103,7 +105,7 @@ class ParticleFilterBatch:
             Ur = np.ascontiguousarray(np.broadcast_to(U.reshape(T, -1, self.nx), (T, self.n_replicates, self.nx)))
         Rn = self.n_replicates
         means = np.zeros((T, Rn, self.nx))
-        covs = np.zeros((T, Rn, self.nx, self.nx)) if self.nx <= 4 else None
+        covs = np.zeros((T, Rn, self.nx, self.nx)) if with_cov else None
         neff = np.zeros((T, Rn))
         flags = np.zeros((T, Rn), dtype=np.uint8)
         lnorm = np.zeros((T, Rn))

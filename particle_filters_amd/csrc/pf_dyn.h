@@ -408,6 +408,10 @@ __global__ void __launch_bounds__(DBS) k_dyn_step(StepParams p) {
         NStream<Real> ns(p.seed, i, nx, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, p.pbase);
         dyn_add_lower<Real>(xo, W + i, S, nx, P + L.LJ, ldiag, ns);
       }
+      if (p.xr_out) {  // the post-resample rows, for the device loop's covariance (pf_cov.h)
+        Real* xr = (Real*)p.xr_out + (int64_t)r * nx * S + i;
+        for (int d = 0; d < nx; ++d) xr[d * S] = xo[d * S];
+      }
     }
     __syncthreads();  // the tile's gathered rows are complete
     const int nfa = 1 + nx + RC.nc;

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/pf_engine.h"
+#include "pf_cov.h"
 #include "pf_order.h"
 #include "../../include/pf_shard.h"
 #include "pf_diag.h"
@@ -224,6 +225,13 @@ struct pf_handle {
   std::vector<ResUndo> res_undo;
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
   bool last_resident = false;  // the last pf_run_device ran k_resident
+  // device-loop covariance for nx > 4 (pf_cov.h): post-resample rows, block partials, sums,
+  // per-replicate arrival counters, and the launch geometry
+  void* xr = nullptr;
+  double* cov_part = nullptr;
+  double* cov_tot = nullptr;
+  unsigned int* cov_cnt = nullptr;
+  CovParams covp{};
   // live kernel timing (pf_set_timing): events recorded on the handle's stream right
   // before the first and after the last filter kernel of each pf_run_device
   bool timing = false;
@@ -519,6 +527,74 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
     if (st) return st;
   }
   if (uniforms || jitter) HIPCHK(hipStreamSynchronize(h->stream));
+  return PF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Device-loop covariance for nx > 4 (pf_cov.h).  Buffers and geometry once per handle: blocks of
+// 4 waves over ~2048 waves per launch (or one block per replicate and block pair for nx > 48).
+// ---------------------------------------------------------------------------
+pf_status ensure_cov(pf_handle* h) {
+  if (h->xr) return PF_OK;
+  CovParams& c = h->covp;
+  c.N = h->N;
+  c.Npad = h->Npad;
+  c.nx = h->nx;
+  c.nb = (h->nx + 15) / 16;
+  c.npairs = c.nb * (c.nb + 1) / 2;
+  c.P = c.npairs * 256 + c.nb * 16 + 1;
+  const int64_t waves_rep = c.nb <= 3 ? std::max<int64_t>(4, 2048 / h->R) : 4;
+  int64_t per = (h->N + waves_rep - 1) / waves_rep;
+  per = std::max<int64_t>(4, (per + 3) / 4 * 4);
+  c.per_wave = (int)per;
+  c.nblk = (int)((h->N + 4 * per - 1) / (4 * per));
+  HIPCHK(hipMalloc(&h->xr, (size_t)h->R * h->nx * h->Npad * h->esz));
+  HIPCHK(hipMalloc((void**)&h->cov_part, (size_t)h->R * c.nblk * c.P * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&h->cov_tot, (size_t)h->R * c.P * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&h->cov_cnt, (size_t)h->R * sizeof(unsigned int)));
+  HIPCHK(hipMemset(h->cov_cnt, 0, (size_t)h->R * sizeof(unsigned int)));
+  c.part = h->cov_part;
+  c.tot = h->cov_tot;
+  c.cnt = h->cov_cnt;
+  return PF_OK;
+}
+
+// Covariance of step s (its predicted rows xs / log-weights lw; the post-resample rows in h->xr,
+// written by the gather that followed) into d_covs[s], from the step's outputs (flag, lse, mean).
+pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, const double* d_means,
+                     const int32_t* d_flags, const double* d_lse, double* d_covs) {
+  CovParams c = h->covp;
+  const int R = h->R;
+  c.xs = xs;
+  c.xr = h->xr;
+  c.lw = lw;
+  c.flag = d_flags + s * R;
+  c.lse = d_lse + s * R;
+  c.mean = d_means + s * R * h->nx;
+  c.cov = d_covs + s * R * h->nx * h->nx;
+  const dim3 blk(256);
+  if (c.nb <= 3) {
+    const dim3 grid((unsigned)c.nblk, (unsigned)R);
+    const size_t lds = 4 * (size_t)c.P * sizeof(double);
+    if (h->esz == 4) {
+      if (c.nb == 1) hipLaunchKernelGGL((k_cov_part<float, 1>), grid, blk, lds, h->stream, c);
+      else if (c.nb == 2) hipLaunchKernelGGL((k_cov_part<float, 2>), grid, blk, lds, h->stream, c);
+      else hipLaunchKernelGGL((k_cov_part<float, 3>), grid, blk, lds, h->stream, c);
+    } else {
+      if (c.nb == 1) hipLaunchKernelGGL((k_cov_part<double, 1>), grid, blk, lds, h->stream, c);
+      else if (c.nb == 2) hipLaunchKernelGGL((k_cov_part<double, 2>), grid, blk, lds, h->stream, c);
+      else hipLaunchKernelGGL((k_cov_part<double, 3>), grid, blk, lds, h->stream, c);
+    }
+  } else {
+    if (c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
+    const dim3 grid((unsigned)c.nblk, (unsigned)R, (unsigned)c.npairs);
+    const size_t lds = 4 * (size_t)(256 + 16 + 1) * sizeof(double);
+    if (h->esz == 4) hipLaunchKernelGGL((k_cov_part<float, 0>), grid, blk, lds, h->stream, c);
+    else hipLaunchKernelGGL((k_cov_part<double, 0>), grid, blk, lds, h->stream, c);
+  }
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_cov_sum, dim3((unsigned)((c.P + 15) / 16), (unsigned)R), dim3(256), 0, h->stream, c);
+  HIPCHK(hipGetLastError());
   return PF_OK;
 }
 
@@ -960,7 +1036,8 @@ void pf_destroy(pf_handle* h) {
   for (double* q : h->lcum)
     if (q) (void)hipFree(q);
   for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
-                  (void*)h->d_replay_b, (void*)h->d_unif})
+                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->cov_part, (void*)h->cov_tot,
+                  (void*)h->cov_cnt})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1173,6 +1250,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   StepParams p = base_params(h);
   p.o_mean = d_means;
   p.o_cov = (h->nx <= 4) ? d_covs : nullptr;
+  // nx > 4: the step's covariance by pf_cov.h after the launch whose gather wrote its post-resample rows
+  const bool cov_loop = d_covs && h->nx > 4;
+  if (cov_loop) {
+    pf_status st = ensure_cov(h);
+    if (st) return st;
+    p.xr_out = h->xr;
+  }
   p.o_neff = d_neff;
   p.o_lse = d_lse;
   p.o_flag = d_flags;
@@ -1195,8 +1279,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
       pf_status st = launch_cdf(h, p);
       if (st) return st;
     }
+    const void *xs_prev = h->x[h->cx], *lw_prev = h->lw[h->clw];  // step s - 1's predicted state
     pf_status st = launch_step(h, p, predict || gather_possible, true, true);
     if (st) return st;
+    if (cov_loop && s >= 1) {
+      st = launch_cov(h, xs_prev, lw_prev, s - 1, d_means, d_flags, d_lse, d_covs);
+      if (st) return st;
+    }
     prev_res = h->epoch++;
     gather_possible = true;
   }
@@ -1214,8 +1303,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     pf_status st = launch_cdf(h, p);
     if (st) return st;
   }
+  const void *xs_last = h->x[h->cx], *lw_last = h->lw[h->clw];
   pf_status st = launch_step(h, p, true, false, true);
   if (st) return st;
+  if (cov_loop) {
+    st = launch_cov(h, xs_last, lw_last, T - 1, d_means, d_flags, d_lse, d_covs);
+    if (st) return st;
+  }
   p.out_step = -1;
   p.out_post_step = T - 1;
   st = launch_finalize(h, p);
@@ -1264,7 +1358,7 @@ pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int3
   if (hipMalloc(&dZ, (size_t)T * R * nz * h->esz) != hipSuccess ||
       (U && hipMalloc(&dU, (size_t)T * R * nx * h->esz) != hipSuccess) ||
       hipMalloc((void**)&dm, (size_t)T * R * nx * sizeof(double)) != hipSuccess ||
-      (covs && nx <= 4 && hipMalloc((void**)&dc, (size_t)T * R * nx * nx * sizeof(double)) != hipSuccess) ||
+      (covs && hipMalloc((void**)&dc, (size_t)T * R * nx * nx * sizeof(double)) != hipSuccess) ||
       hipMalloc((void**)&dn, (size_t)T * R * sizeof(double)) != hipSuccess ||
       hipMalloc((void**)&dl, (size_t)T * R * sizeof(double)) != hipSuccess ||
       hipMalloc((void**)&df, (size_t)T * R * sizeof(int32_t)) != hipSuccess)

@@ -404,6 +404,9 @@ struct StepParams {
   void* wbuf;
   int64_t wrows;
   int a_diag, lq_diag, lj_diag;
+  // device-loop covariance for nx > 4 (pf_cov.h): a gathering launch also writes its post-resample
+  // (post-jitter) rows here, [R][NX][Npad]; null: not wanted
+  void* xr_out;
 };
 
 struct Head {

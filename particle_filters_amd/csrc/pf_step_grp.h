@@ -592,6 +592,11 @@ k_step_grp(StepParams p) {
       aux0 += 1.0;
 #pragma unroll
       for (int j = 0; j < PER; ++j) auxj[j] += (double)x[j];
+      if (p.xr_out) {  // the post-resample rows, for the device loop's covariance (pf_cov.h)
+        Real* xr = (Real*)p.xr_out + (int64_t)r * NX * p.Npad;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) xr[(int64_t)(q * PER + j) * p.Npad + i] = x[j];
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < PER; ++j) x[j] = x_in[(int64_t)(q * PER + j) * p.Npad + i];

@@ -298,7 +298,7 @@ class ParticleFilter:
         self.predict(u)
         return self.update(z)
 
-    def run(self, Z, U=None, *, first_update_only: bool = False):
+    def run(self, Z, U=None, *, first_update_only: bool = False, with_cov: bool = True):
         """The reference driver loop ``for t: state = step(Z[t], U[t])`` (or ``update(Z[0])``
         first when ``first_update_only``) executed on the GPU with no host sync inside T.
         Device RNG only (host replay needs the per-step resample decisions on the host).
@@ -311,7 +311,7 @@ class ParticleFilter:
         T = Z.shape[0]
         Uc = None if U is None else np.ascontiguousarray(np.asarray(U, float).reshape(T, self.nx))
         means = np.zeros((T, 1, self.nx))
-        covs = np.zeros((T, 1, self.nx, self.nx)) if self.nx <= 4 else None
+        covs = np.zeros((T, 1, self.nx, self.nx)) if with_cov else None
         neff = np.zeros((T, 1))
         flags = np.zeros((T, 1), dtype=np.uint8)
         lnorm = np.zeros((T, 1))

@@ -56,7 +56,7 @@ def margins(w, U, idx):
 
 
 def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_pre, we_pre, neff_e, neff_e0,
-             flag_e, mean_e, xe_post, scale, bm24=True, tie_floor=1e-7, exp_err=2.0 ** -22, K=8):
+             flag_e, mean_e, xe_post, scale, bm24=True, tie_floor=1e-7, exp_err=2.0 ** -22, K=8, cov_e=None):
     """Compare one engine step with the oracle's from the same state.  Returns a dict of measured
     quantities (see module docstring); tolerances are applied by ``check``."""
     N, nx = x0.shape
@@ -76,10 +76,14 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     out["flag_e"], out["flag_o"] = bool(flag_e), bool(o.last_resampled)
     out["near_threshold"] = bool(abs(o.last_neff - thresh * N) / N < 1e-3)
     out["resampled"] = bool(flag_e)
+    out["dcov"] = 0.0
     if not flag_e:
         out["dx_post"] = float(np.max(np.abs(xe_post - xe_pre)))  # no resample: the state is x'_e itself
         mo = st.mean if not o.last_resampled else np.average(o.pre_x, axis=0, weights=o.pre_w)
         out["dmean"] = float(np.max(np.abs(mean_e - mo)))
+        if cov_e is not None:  # pf.py:266-267 on the weighted predicted particles
+            co = np.atleast_2d(np.cov(o.pre_x.T, aweights=o.pre_w, bias=True))
+            out["dcov"] = float(np.max(np.abs(cov_e - co)) / max(np.max(np.abs(co)), 1e-300))
         out["dmean_oracle"] = out["dmean"]
         out["n_anc_self_mismatch"] = out["n_anc_diff"] = 0
         out["max_margin_diff"] = 0.0
@@ -118,16 +122,25 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
         hit = np.max(np.abs(xe_post[todo] - (xe_pre[cand[todo]] + jit[todo])), axis=1) <= tol_copy
         sel = np.nonzero(todo)[0][hit]
         idx_e[sel] = cand[sel]
-    # a near-tie may also skip particles of (numerically) zero weight, far away in index: the few
-    # slots not matched near the oracle's ancestor are looked up among all predicted particles
+    # a near-tie may also skip particles of (numerically) zero weight, far away in index: the slots
+    # not matched near the oracle's ancestor are looked up among all predicted particles (exact
+    # row lookup; with jitter, a scan of at most 256 slots)
     rest = np.nonzero(idx_e < 0)[0]
-    if 0 < rest.size <= 256:
+    if rest.size and not reg:
+        rows = {}
+        for j, key in enumerate(map(bytes, np.ascontiguousarray(xe_pre))):
+            rows.setdefault(key, []).append(j)
         for i in rest:
-            m = np.nonzero(np.max(np.abs(xe_pre + jit[i] - xe_post[i]), axis=1) <= tol_copy)[0]
+            m = np.asarray(rows.get(bytes(np.ascontiguousarray(xe_post[i])), []), dtype=np.int64)
             if m.size:  # the copy whose oracle CDF interval is nearest the slot's position
                 lo = np.where(m > 0, cdf_o[np.maximum(m - 1, 0)], 0.0)
-                dm = np.maximum(0.0, np.maximum(lo - pos[i], pos[i] - cdf_o[m]))
-                idx_e[i] = m[np.argmin(dm)]
+                idx_e[i] = m[np.argmin(np.maximum(0.0, np.maximum(lo - pos[i], pos[i] - cdf_o[m])))]
+    elif 0 < rest.size <= 256:
+        for i in rest:
+            m = np.nonzero(np.max(np.abs(xe_pre + jit[i] - xe_post[i]), axis=1) <= tol_copy)[0]
+            if m.size:
+                lo = np.where(m > 0, cdf_o[np.maximum(m - 1, 0)], 0.0)
+                idx_e[i] = m[np.argmin(np.maximum(0.0, np.maximum(lo - pos[i], pos[i] - cdf_o[m])))]
     out["n_unmatched"] = int(np.sum(idx_e < 0))
     diff = (idx_e >= 0) & (idx_e != idx_o)
     d = dist(np.maximum(idx_e, 0))
@@ -140,10 +153,13 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     out["dmean_oracle"] = float(np.max(np.abs(mean_e - st.mean)))
     out["dx_post"] = float(np.max(np.abs(xe_post - forced)))
     out["n_anc_self_mismatch"] = out["n_unmatched"]
+    if cov_e is not None:  # pf.py:266-267 on the resampled set (uniform weights), the engine's ancestors
+        co = np.atleast_2d(np.cov(forced.T, bias=True))
+        out["dcov"] = float(np.max(np.abs(cov_e - co)) / max(np.max(np.abs(co)), 1e-300))
     return out
 
 
-def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5):
+def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5, tol_cov=2e-5):
     """Tolerances (stated in the test module): particles tol_x x scale (fp32 rounding of one step),
     weights' TV distance tol_tv, Neff rel tol_neff, decisions identical unless Neff is within
     1e-3 N of the threshold; every post-step slot is a copy of one of the engine's predicted
@@ -160,6 +176,7 @@ def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5):
     if c["resampled"]:
         assert c["max_margin_diff"] <= c["band"], c
     assert c["dmean"] <= tol_mean * scale, c
+    assert c["dcov"] <= tol_cov, c
     assert c["dx_post"] <= 2 * tol_x * scale, c
 
 
@@ -167,4 +184,4 @@ def fmt(t, c):
     return (f"t={t:4d} res={int(c['flag_e'])}/{int(c['flag_o'])} dx_pre={c['dx_pre']:.2e} tvw={c['tv_w']:.2e} "
             f"dcdf={c['dcdf']:.2e} dNeff={c['neff_rel']:.2e} dmean={c['dmean']:.2e} (vs oracle's own "
             f"ancestors {c['dmean_oracle']:.2e}) anc_diff={c['n_anc_diff']} max_margin={c['max_margin_diff']:.2e} "
-            f"band={c.get('band', 0.0):.2e} unmatched={c['n_anc_self_mismatch']}")
+            f"band={c.get('band', 0.0):.2e} unmatched={c['n_anc_self_mismatch']} dcov/|cov|={c['dcov']:.2e}")

@@ -1,0 +1,137 @@
+"""The posterior covariance in the device loop for any nx (csrc/pf_cov.h), -m gpu.
+
+The reference computes ``cov = np.cov(particles.T, aweights=w, bias=True)`` of the state every
+update returns (pf.py:266-267).  For nx > 4 the device loop (``run()``) computes it per step with
+MFMA block products over the reported rows (the post-resample rows the gather wrote, or the
+weighted predicted rows).  Stated tolerances:
+
+* fp64 ``run()`` (device RNG) against the oracle driven by the engine's Philox draws
+  (oracle/sir_philox.py PhiloxSIROracle = oracle/pf_oracle.py SIROracle, pinned bit for bit to the
+  reference's own outputs, tests/test_oracle_golden.py): identical decisions, means rtol 1e-9,
+  covariances within 1e-9 x max|cov| of the step - L96 d = 40 (compiled lane-group step, three
+  16-blocks), the joint MAT model (nx = 16, 2 replicates), L96 nx = 12 on the runtime-shape
+  kernels, a 50-D linear system (nx > 48: one block pair per workgroup) and multinomial resampling
+  with jitter (the covariance of the post-jitter rows);
+* fp32 ``run()`` against the same run's fp64 two-pass moments of its own final state
+  (``pf_moments``): within 2e-5 x max|cov| (fp32 MFMA partial sums, fp64 beyond);
+* the reference's own runs (tests/golden/pf_runs.npz l96 / mat covs) are matched by the step API
+  in replay mode (tests/test_gpu_parity.py, rtol 1e-8); run() cannot replay PCG64 draws, whose
+  consumption depends on the decisions, hence the Philox-driven oracle here.
+"""
+
+import numpy as np
+import pytest
+
+import bench
+from particle_filters_amd import _native as NV, models as M
+from particle_filters_amd.batch import ParticleFilterBatch
+from oracle import sir_philox as SP, ssm_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert NV.device_count() > 0, "no HIP device visible: -m gpu tests must run on an MI355X"
+
+
+def oracle_run(ssm, Q, R, Z, *, N, seed, rep, mean0, cov0, method="systematic", reg=False, bm24=False):
+    o = SP.PhiloxSIROracle(ssm.g_vec, ssm.h_vec, Q, R, seed=seed, rep=rep, bm24=bm24, Np=N, resample_method=method,
+                           regularize_after_resample=reg, vectorized=True)
+    o.initialize(np.asarray(mean0, float), np.asarray(cov0, float))
+    T = Z.shape[0]
+    out = dict(means=np.zeros((T, o.nx)), covs=np.zeros((T, o.nx, o.nx)), flags=np.zeros(T, bool))
+    for t in range(T):
+        st = o.step(np.atleast_1d(Z[t]))
+        out["means"][t], out["covs"][t], out["flags"][t] = st.mean, st.cov, o.last_resampled
+    return out
+
+
+def check_vs_oracle(g, h, ssm, Q, R, Z, *, N, n_rep=1, seed=5, mean0, cov0, method="systematic", reg=False,
+                    kernel_path="auto", tol=1e-9):
+    b = ParticleFilterBatch(g, h, Q, R, Np=N, n_replicates=n_rep, seed=seed, precision="fp64", resample_method=method,
+                            regularize_after_resample=reg, kernel_path=kernel_path)
+    b.initialize(mean0, cov0)
+    r = b.run(Z)
+    b.close()
+    assert r.covs is not None
+    for k in range(n_rep):
+        o = oracle_run(ssm, Q, R, Z, N=N, seed=seed, rep=k, mean0=mean0, cov0=cov0, method=method, reg=reg)
+        assert np.array_equal(r.flags[:, k], o["flags"])
+        np.testing.assert_allclose(r.means[:, k], o["means"], rtol=tol, atol=tol)
+        scale = np.max(np.abs(o["covs"]), axis=(1, 2), keepdims=True)
+        err = np.max(np.abs(r.covs[:, k] - o["covs"]) / scale)
+        print(f"replicate {k}: max |dcov| / max|cov| = {err:.2e}, resamples {int(o['flags'].sum())}")
+        assert err <= tol
+        assert np.allclose(r.covs[:, k], np.swapaxes(r.covs[:, k], 1, 2), rtol=0, atol=0)  # symmetric
+    assert r.flags.any()
+    return r
+
+
+def test_l96_d40_compiled_step():
+    wl = bench.WORKLOADS["l96"]()
+    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(15, 0)
+    check_vs_oracle(g, h, wl.oracle_ssm(), np.asarray(Q, float), np.asarray(R, float), np.asarray(Z, float), N=2000,
+                    mean0=mean0, cov0=cov0)
+
+
+def test_mat_joint_two_replicates():
+    wl = bench.WORKLOADS["mat"]()
+    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(10, 0)
+    check_vs_oracle(g, h, wl.oracle_ssm(), np.asarray(Q, float), np.asarray(R, float), np.asarray(Z, float), N=1500,
+                    n_rep=2, mean0=mean0, cov0=cov0)
+
+
+def test_l96_nx12_runtime_shape(golden_l96):
+    truth = golden_l96["truth2"]
+    H_idx = golden_l96["H_idx2"]
+    rs = np.random.default_rng(5)
+    Z = truth[1:16, H_idx] + 0.5 * rs.standard_normal((15, H_idx.size))
+    ssm = ssm_oracle.lorenz96(nx=12, F=6.0, dt=0.02, obs_fraction=3, obs_error_std=0.5, q_std=0.1)
+    g, h = M.L96Transition(6.0, 0.02, 12), M.SelectObservation(H_idx, 12)
+    check_vs_oracle(g, h, ssm, ssm.Q, ssm.R, Z, N=1200, mean0=truth[0] + 0.3, cov0=np.eye(12), kernel_path="runtime")
+
+
+def _linear50():
+    nx, nz = 50, 10
+    rs = np.random.default_rng(9)
+    A = 0.9 * np.eye(nx) + 0.01 * rs.standard_normal((nx, nx))
+    H = rs.standard_normal((nz, nx)) / np.sqrt(nx)
+    Q = 0.05 * np.eye(nx)
+    R = 0.2 * np.eye(nz)
+    x = np.zeros(nx)
+    Z = np.zeros((12, nz))
+    for t in range(12):
+        x = A @ x + np.sqrt(0.05) * rs.standard_normal(nx)
+        Z[t] = H @ x + np.sqrt(0.2) * rs.standard_normal(nz)
+    return ssm_oracle.linear(A, H, Q, R), M.LinearTransition(A), M.LinearObservation(H), Z
+
+
+@pytest.mark.parametrize("method,reg", [("systematic", False), ("multinomial", True)])
+def test_linear_50d_pair_grid(method, reg):
+    """nx = 50 > 48: the block-pair grid of k_cov_part (10 pairs of 16-blocks); multinomial with
+    jitter: the covariance of the post-jitter rows the gather wrote."""
+    ssm, g, h, Z = _linear50()
+    check_vs_oracle(g, h, ssm, ssm.Q, ssm.R, Z, N=1500, mean0=np.zeros(50), cov0=0.5 * np.eye(50), method=method,
+                    reg=reg)
+
+
+@pytest.mark.parametrize("name,T", [("l96", 12), ("mat", 8)])
+def test_fp32_run_cov_vs_final_moments(name, T):
+    """fp32 engine: the last step's device-loop covariance equals the exact two-pass fp64 moments
+    of the final state (pf_moments) to fp32 MFMA accuracy."""
+    wl = bench.WORKLOADS[name]()
+    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(T, 0)
+    b = ParticleFilterBatch(g, h, Q, R, Np=wl.n_particles, n_replicates=wl.replicates, seed=42)
+    b.initialize(mean0, cov0)
+    r = b.run(np.asarray(Z, float))
+    nx = b.nx
+    m = np.empty((wl.replicates, nx))
+    c = np.empty((wl.replicates, nx, nx))
+    NV.check(NV.load().pf_moments(b.handle, NV.dptr(m), NV.dptr(c)))
+    b.close()
+    scale = np.max(np.abs(c), axis=(1, 2), keepdims=True)
+    err = float(np.max(np.abs(r.covs[-1] - c) / scale))
+    print(f"{name}: fp32 device-loop cov vs two-pass fp64 moments of the final state: {err:.2e}")
+    assert err <= 2e-5
+    np.testing.assert_allclose(r.means[-1], m, rtol=1e-5, atol=1e-5 * np.max(np.abs(m)))

@@ -22,6 +22,8 @@ Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the 
                             engine's ancestor: a near-tie of the two CDFs, nothing else
   posterior mean            <= 1e-5 x scale against the oracle's particles under the engine's
                             ancestors
+  posterior covariance      <= 2e-5 x max|cov| against np.cov of the same set (pf.py:266-267;
+                            nx > 4: the device loop's MFMA covariance, csrc/pf_cov.h)
 The kernels covered: k_resident (config 2, N = 1e6), k_step_grp<float,40,10> (config 3, N = 1e5),
 k_step_grp<float,16,25> (config 4, 8 x 1e5: lane-local transition, v_rcp_f32 acoustic terms,
 rounds-aware tiles), k_step<float,1,1> over 64 x 1e6 (sv64) and k_step<double,1,1> (the fp64 line,
@@ -92,7 +94,7 @@ def chain(name, T, n_bound=20, reps=None, precision="fp32", expect_resident=None
             c = TF.one_step(ssm, Q, R, seed=42, rep=k, epoch=rs["epoch"], thresh=0.5, method="systematic", reg=False,
                             x0=x0[k], w0=w0[k], z=Z[t], xe_pre=xe_pre[k], we_pre=we_pre[k], neff_e=r.neff[0, k],
                             neff_e0=r0.neff[0, k], flag_e=r.flags[0, k], mean_e=r.means[0, k], xe_post=xe_post[k],
-                            scale=scale, bm24=bm24, **(step_kw or {}))
+                            scale=scale, bm24=bm24, cov_e=r.covs[0, k], **(step_kw or {}))
             print(f"{name} rep {k}: " + TF.fmt(t, c))
             TF.check(c, scale=scale, **(tol or {}))
             results.append(c)
@@ -145,5 +147,5 @@ def test_step_sv64():
 def test_step_fp64_sv_config2():
     """k_step<double,1,1> (the fp64 line), config 2, T = 200: fp64 arithmetic, 32-bit Box-Muller."""
     chain("sv", 200, n_bound=10, precision="fp64",
-          tol=dict(tol_x=1e-12, tol_mean=1e-11, tol_neff=1e-10, tol_tv=1e-10),
+          tol=dict(tol_x=1e-12, tol_mean=1e-11, tol_neff=1e-10, tol_tv=1e-10, tol_cov=1e-10),
           step_kw=dict(tie_floor=1e-12, exp_err=1e-15))
