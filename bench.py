@@ -486,7 +486,31 @@ def cpu_baseline_numpy(wl, Z, mean0, cov0):
 
 
 def oracle_threads():
-    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    """Threads of the C/OpenMP leg: this process's CPU share.  On the GPU pool a one-GPU box is
+    allotted 16 host CPUs (OMP_NUM_THREADS is set to it there); os.cpu_count() reports the whole
+    node, whose other cores serve other GPUs' jobs.  Without OMP_NUM_THREADS: the affinity set."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, env or len(os.sched_getaffinity(0)))
+
+
+def cpu_c1_full_run():
+    """the full BASELINE config 1 run on the faithful restatement (bit-identical
+    to the reference): SV log-squared wiring, N = 1000, T = 999 (simulate_sv_1d n = 1000 seed 42),
+    initialize([X0], [[0.5]]), systematic at 0.5 N, PF seed 42, 1 core."""
+    from oracle import pf_oracle, ssm_oracle
+    from particle_filters_amd import simulators as S
+
+    d = S.simulate_sv_1d(1000, ALPHA, SIGMA, BETA, seed=42)
+    Z = np.log(d.Y[1:] ** 2)[:, None]
+    ssm = ssm_oracle.sv_logsq(ALPHA, SIGMA, BETA)
+    t0 = time.perf_counter()
+    o = pf_oracle.build_and_run(ssm, Z, Np=1000, seed=42, mean0=[d.X[0]], cov0=[[0.5]], vectorized=False)
+    dt = time.perf_counter() - t0
+    rmse = float(np.sqrt(np.mean((o["means"][:, 0] - d.X[1:]) ** 2)))
+    return {"value": 1000 * len(Z) / dt, "unit": "particle-steps/s", "cores": 1, "kind": "port", "seconds": dt,
+            "rmse_vs_truth": rmse,
+            "sample": f"BASELINE config 1 in full: SV log-squared, N=1000, T={len(Z)}, seed 42, faithful per-particle "
+                      f"restatement (oracle/pf_oracle.py, bit-identical to the reference), {dt:.2f} s"}
 
 
 def rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, eng_means, eng_flags, precision):
@@ -580,6 +604,8 @@ def main():
     ap.add_argument("--spawn", action="store_true", help="launch the rank processes even for --gpus 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref", action="store_true", help="skip the rmse_vs_ref oracle leg")
+    ap.add_argument("--no-cov", action="store_true",
+                    help="do not compute the per-step posterior covariance (the reference computes it)")
     args = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
         sys.exit(spawn_ranks(args.gpus))
@@ -643,6 +669,9 @@ def main():
     NV.check(lib.pf_set_timing(pf.handle, 1), "pf_set_timing")
 
     out_store = torch.zeros(max(W, K) * Rl * (nx + 3), dtype=torch.float64, device=dev)
+    # the posterior covariance of every step (pf.py:266-267, part of the reference's reported state);
+    # --no-cov drops it (named in config)
+    cov_store = None if args.no_cov else torch.zeros(max(W, K) * Rl * nx * nx, dtype=torch.float64, device=dev)
 
     def outs(T):
         """The run's outputs as views of ONE contiguous float64 buffer (means [T][R][nx], Neff,
@@ -671,7 +700,8 @@ def main():
 
     def run_args(dzz, T, o):  # the ctypes arguments, built outside the timed region
         means, neff, flags, lnorm, _ = o
-        return (pf.handle, NV.C.c_void_p(dzz.data_ptr()), None, T, 0, NV.C.c_void_p(means.data_ptr()), None,
+        covs = None if cov_store is None else NV.C.c_void_p(cov_store.data_ptr())
+        return (pf.handle, NV.C.c_void_p(dzz.data_ptr()), None, T, 0, NV.C.c_void_p(means.data_ptr()), covs,
                 NV.C.c_void_p(neff.data_ptr()), NV.C.c_void_p(flags.data_ptr()), NV.C.c_void_p(lnorm.data_ptr()))
 
     def run(a):
@@ -768,6 +798,15 @@ def main():
             except Exception as e:
                 errors.append(f"numpy restatement: {e!r}")
                 log("cpu numpy baseline failed:", repr(e))
+            if wl.name in ("sv", "sv64"):
+                try:
+                    c1 = cpu_c1_full_run()
+                    if cpu is None:
+                        cpu = {"value": None, "unit": "particle-steps/s", "cores": 1, "kind": "port"}
+                    cpu["c1_full_run"] = c1
+                except Exception as e:
+                    errors.append(f"C1 full run: {e!r}")
+                    log("C1 full run failed:", repr(e))
             if errors and cpu is not None:
                 cpu["errors"] = errors
         ref = None
@@ -783,8 +822,14 @@ def main():
                     ref["mc_sd_rmse_over_replicates"] = sd
                     ref["abs_diff_in_mc_sd"] = ref["abs_diff"] / sd if sd > 0 else None
                 if cpu is not None and wl.nx == 1 and "ref_particle_steps_per_s" in ref:
+                    th = ref["ref_threads"]
                     cpu["c_openmp"] = {"value": ref["ref_particle_steps_per_s"], "unit": "particle-steps/s",
-                                       "cores": ref["ref_threads"], "kind": "port",
+                                       "cores": th, "host_cores": os.cpu_count(),
+                                       "cores_note": "this box's CPU share (OMP_NUM_THREADS of the GPU pool); the "
+                                                     "node's other cores serve its other GPUs",
+                                       "extrapolated_all_host_cores": ref["ref_particle_steps_per_s"] *
+                                       (os.cpu_count() or th) / th,
+                                       "kind": "port",
                                        "sample": f"the rmse_vs_ref run: {Np:.0e} particles x {W + K} steps, C "
                                                  f"restatement (oracle/sir_philox.c, fp64), {ref['ref_seconds']:.1f} s"}
             except Exception as e:
@@ -809,7 +854,10 @@ def main():
                        "kernel_path": "runtime-shape (pf_dyn.h)" if dyn else "compiled shape",
                        "parallelism": f"replicates x{world} (independent filters per GPU"
                                       + (", RCCL all-gather of summaries)" if dist else ")"),
-                       "geometry": {"tiles": G, "tile": tile, "lds_bytes": lds}},
+                       "geometry": {"tiles": G, "tile": tile, "lds_bytes": lds},
+                       "posterior_cov": "none (--no-cov)" if args.no_cov else
+                       ("every step, in the step kernel's records" if nx <= 4 else
+                        "every step, MFMA block products over the reported rows (csrc/pf_cov.h)")},
             "rmse": rmse[0],
             "rmse_all_replicates": rmse,
             "rmse_vs_ref": ref,
