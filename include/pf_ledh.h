@@ -82,11 +82,20 @@ pf_status pf_ledh_get_weights(pf_ledh_handle* h, double* weights);
 pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const double* weights);
 
 /* The whole T loop on the device with no host synchronisation inside T:
- * Ps [T][nx][nx] tracker covariances, Z [T][nz], U [T][nx] or NULL.  Noise PF_NOISE_NONE or
- * PF_NOISE_DEVICE; resampling uniforms from Philox.  Outputs (host, nullable): means [T][nx],
+ * Ps [T][nx][nx] tracker covariances, Z [T][nz], U [T][nx] or NULL.  Noise PF_NOISE_NONE,
+ * PF_NOISE_DEVICE (resampling uniforms from Philox) or PF_NOISE_HOST (the draws set by
+ * pf_ledh_set_run_replay for a run of this T).  Outputs (host, nullable): means [T][nx],
  * covs [T][nx][nx], ess [T], flags [T]. */
 pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T,
                       int32_t noise, double* means, double* covs, double* ess, uint8_t* flags);
+
+/* Replayed draws for the NEXT run of T steps (pf_ledh_run / pf_edh_run / pf_ledh_run_ekf with
+ * noise PF_NOISE_HOST): step t's process noise v_t [N][nx] (the process_noise_sampler draw,
+ * ledh.py:109-116) and its resampling uniform U_t (the rng.random() of systematic_resample,
+ * ledh.py:28; read only when step t resamples).  The reference's generator consumes U_t only on
+ * resampling steps, so a caller replaying its stream lays the draws out with the decisions it
+ * expects (and checks the run's flags against them).  noise [T][N][nx], uniforms [T]; copied. */
+pf_status pf_ledh_set_run_replay(pf_ledh_handle* h, const double* noise, const double* uniforms, int64_t T);
 
 /* The Gaussian tracker on the device: the additive-noise EKF of extended_kalman_filter.py:164-241
  * (predict x = g(x), P = G P G^T + Qt; update with S = H P H^T + Rt, K = P H^T S^-1, P = (I - K H) P)

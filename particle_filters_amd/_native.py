@@ -147,6 +147,7 @@ SIGNATURES = {
     "pf_ledh_ekf_sequence": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, C.c_int64, _dp, _dp, _dp]),
     "pf_ledh_run_ekf": (C.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp,
                                     C.POINTER(C.c_uint8), _dp, _dp]),
+    "pf_ledh_set_run_replay": (C.c_int32, [_vp, _dp, _dp, C.c_int64]),
     "pf_ledh_stream": (_vp, [_vp]),
     "pf_ledh_synchronize": (C.c_int32, [_vp]),
     "pf_ledh_shared_path": (C.c_int32, [_vp]),

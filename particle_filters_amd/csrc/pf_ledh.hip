@@ -290,6 +290,9 @@ struct pf_ledh_handle {
   unsigned long long *fwords = nullptr, *fpart = nullptr, *fcpart = nullptr;
   unsigned int* ferr = nullptr;
   double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
+  // replayed draws for the next run (pf_ledh_set_run_replay): noise [T][N][nx], U [T]
+  double *rp_noise = nullptr, *rp_unif = nullptr;
+  int64_t rp_T = 0;
 };
 
 namespace {
@@ -578,7 +581,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
-                    h->xbar})
+                    h->xbar, h->rp_noise, h->rp_unif})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)h->fwords, (void*)h->fpart, (void*)h->fcpart, (void*)h->ferr})
     if (p) (void)hipFree(p);
@@ -772,7 +775,10 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
   const bool edh = h->algo == 1;
   if (edh && !ekf && !Xb) return lfail(PF_E_ARG, "EDH run needs the tracker's past means");
   if (!h->initialized) return lfail(PF_E_NOT_INITIALIZED, "Filter not initialized.");
-  if (noise != PF_NOISE_NONE && noise != PF_NOISE_DEVICE) return lfail(PF_E_ARG, "run: noise must be NONE or DEVICE");
+  if (noise == PF_NOISE_HOST && h->rp_T != T)
+    return lfail(PF_E_ARG, "run: PF_NOISE_HOST needs pf_ledh_set_run_replay with the run's T");
+  if (noise < PF_NOISE_NONE || noise > PF_NOISE_DEVICE) return lfail(PF_E_ARG, "run: bad noise mode");
+  const bool replay = noise == PF_NOISE_HOST;
   if (T <= 0) return PF_OK;
   LCHK(hipSetDevice(h->device));
   const int nx = h->nx, nz = h->nz;
@@ -886,8 +892,10 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       }
       if (h->fused_nbk > 0 && dTab) {  // the whole step in one launch (pf_ledh_fused.h)
         FusedParams fp;
-        fp.f = flow_params(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr);
+        fp.f = flow_params(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise,
+                           replay ? h->rp_noise + t * h->N * nx : nullptr, nullptr);
         fp.f.table = dTab + t * tsz;
+        fp.rp_unif = replay ? h->rp_unif + t : nullptr;
         fp.f.epoch = ++h->epoch;
         fp.ep_res = ++h->epoch;
         fp.x_res = h->x;
@@ -917,9 +925,10 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         std::swap(h->mean, h->mean_prev);
         continue;
       }
-      st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise, nullptr, nullptr, de + t,
-                        df + t, dTab ? dTab + t * tsz : nullptr);
-      if (st == PF_OK) st = enqueue_finish(h, nullptr, dm + t * nx, dc + t * nx * nx);
+      st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise,
+                        replay ? h->rp_noise + t * h->N * nx : nullptr, nullptr, de + t, df + t,
+                        dTab ? dTab + t * tsz : nullptr);
+      if (st == PF_OK) st = enqueue_finish(h, replay ? h->rp_unif + t : nullptr, dm + t * nx, dc + t * nx * nx);
     }
     if (order) order->end();
     if (ekf) (void)hipStreamSynchronize(h->side);
@@ -952,6 +961,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
   } while (false);
   cleanup();
   h->pending = false;
+  h->rp_T = 0;  // a replay source serves one run
   return st;
 }
 
@@ -1011,6 +1021,22 @@ pf_status pf_ledh_ekf_sequence(pf_ledh_handle* h, const double* x0, const double
   for (double* p : {dE, dZ, dP})
     if (p) (void)hipFree(p);
   return st;
+}
+
+pf_status pf_ledh_set_run_replay(pf_ledh_handle* h, const double* noise, const double* uniforms, int64_t T) {
+  if (!h || !noise || !uniforms || T <= 0) return lfail(PF_E_ARG, "null argument");
+  LCHK(hipSetDevice(h->device));
+  LCHK(hipStreamSynchronize(h->stream));
+  for (double* p : {h->rp_noise, h->rp_unif})
+    if (p) LCHK(hipFree(p));
+  h->rp_noise = h->rp_unif = nullptr;
+  h->rp_T = 0;
+  LCHK(hipMalloc((void**)&h->rp_noise, (size_t)T * h->N * h->nx * 8));
+  LCHK(hipMalloc((void**)&h->rp_unif, (size_t)T * 8));
+  LCHK(hipMemcpy(h->rp_noise, noise, (size_t)T * h->N * h->nx * 8, hipMemcpyHostToDevice));
+  LCHK(hipMemcpy(h->rp_unif, uniforms, (size_t)T * 8, hipMemcpyHostToDevice));
+  h->rp_T = T;
+  return PF_OK;
 }
 
 void* pf_ledh_stream(pf_ledh_handle* h) { return h ? (void*)h->stream : nullptr; }

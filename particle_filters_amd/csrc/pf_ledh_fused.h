@@ -69,6 +69,7 @@ struct FusedParams {
   unsigned long long phase0;     // phase word base of this launch
   double ratio;
   uint32_t ep_res;               // Philox epoch of the resampling offset U
+  const double* rp_unif;         // replayed U of this step (host draw stream) or null (Philox)
   int nbk, ppb;
 };
 
@@ -216,7 +217,8 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   __shared__ double slice[FNST * FPPB];
   __shared__ int anc[FMC];
   __shared__ int krange[2];
-  const double U = flag ? uniform53(p.f.seed, 0u, 0u, p.ep_res) : 0.0;  // ledh.py:28 (Philox, as k_gather)
+  // ledh.py:28: the step's U (Philox, as k_gather; or the replayed host draw)
+  const double U = flag ? (p.rp_unif ? *p.rp_unif : uniform53(p.f.seed, 0u, 0u, p.ep_res)) : 0.0;
   const double dN = (double)N;
   // first workgroup whose last CDF value exceeds pos (the last one if none)
   auto src_block = [&](double pos) {

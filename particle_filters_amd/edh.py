@@ -139,7 +139,7 @@ class EDHFlowPF(LEDHFlowPF):
         return self._new_state(mean, cov, {"condition_numbers": conds})
 
     def run(self, state: PFState, Z: Array, U: Optional[Array] = None, *, process_noise: str = "device",
-            tracker_seq: Optional[tuple] = None, tracker: str = "host") -> LEDHRunResult:
+            tracker_seq: Optional[tuple] = None, tracker: str = "host", replay=None) -> LEDHRunResult:
         """The driver loop ``for t: state = step(state, Z[t])`` on the device with no host
         synchronisation inside T.  ``tracker="host"``: the tracker object is run ahead over Z
         (predict / get_past_mean / update, the same call sequence as the loop — it never sees
@@ -147,16 +147,14 @@ class EDHFlowPF(LEDHFlowPF):
         ``tracker="device"``: an EKFTracker over this filter's models runs on the GPU and
         also yields the past means.  Process noise is Philox times chol(Q) (``"device"``) or
         zero (``"none"``); resampling uniforms come from Philox."""
-        if process_noise not in ("device", "none"):
-            raise ValueError("process_noise must be 'device' or 'none'")
         if tracker not in ("host", "device"):
             raise ValueError("tracker must be 'host' or 'device'")
         if tracker == "device":
-            return super().run(state, Z, U, process_noise=process_noise, tracker="device")
+            return super().run(state, Z, U, process_noise=process_noise, tracker="device", replay=replay)
         self._adopt(state)
         Z = np.ascontiguousarray(np.asarray(Z, float).reshape(-1, self.nz))
         T = Z.shape[0]
-        noise = N.PF_NOISE_DEVICE if process_noise == "device" else N.PF_NOISE_NONE
+        noise = self._noise_mode(process_noise, replay, T)
         if tracker_seq is None:
             Ps = np.empty((T, self.nx, self.nx))
             Xb = np.empty((T, self.nx))

@@ -281,8 +281,23 @@ class LEDHFlowPF:
                                               Z.shape[0], N.dptr(Ps), None, None), "pf_ledh_ekf_sequence")
         return Ps
 
+    def _noise_mode(self, process_noise: str, replay, T: int) -> int:
+        """process_noise "device" (Philox), "none", or "host": replay = (V [T][N][nx], U [T]), the
+        reference's draws (the process_noise_sampler's per step, and systematic_resample's
+        rng.random() at the steps that resample), consumed by the device loop in that order."""
+        if process_noise not in ("device", "none", "host"):
+            raise ValueError("process_noise must be 'device', 'none' or 'host'")
+        if process_noise != "host":
+            return N.PF_NOISE_DEVICE if process_noise == "device" else N.PF_NOISE_NONE
+        if replay is None:
+            raise ValueError("process_noise='host' needs replay=(V [T][N][nx], U [T])")
+        V = np.ascontiguousarray(np.asarray(replay[0], float).reshape(T, self.n, self.nx))
+        Uu = np.ascontiguousarray(np.asarray(replay[1], float).reshape(T))
+        N.check(N.load().pf_ledh_set_run_replay(self._h, N.dptr(V), N.dptr(Uu), T), "pf_ledh_set_run_replay")
+        return N.PF_NOISE_HOST
+
     def run(self, state: PFState, Z: Array, U: Optional[Array] = None, *, process_noise: str = "device",
-            tracker_covs: Optional[Array] = None, tracker: str = "host") -> LEDHRunResult:
+            tracker_covs: Optional[Array] = None, tracker: str = "host", replay=None) -> LEDHRunResult:
         """The driver loop ``for t: state = step(state, Z[t])`` on the device with no host
         synchronisation inside T.  ``tracker="host"``: the tracker object is run ahead over Z
         (predict/update, the same call sequence as the loop — it never sees the particles)
@@ -291,14 +306,12 @@ class LEDHFlowPF:
         to the final posterior afterwards.  Process noise is Philox times chol(Q)
         (``"device"``) or zero (``"none"``, the reference default); resampling uniforms come
         from Philox."""
-        if process_noise not in ("device", "none"):
-            raise ValueError("process_noise must be 'device' or 'none'")
         if tracker not in ("host", "device"):
             raise ValueError("tracker must be 'host' or 'device'")
         self._adopt(state)
         Z = np.ascontiguousarray(np.asarray(Z, float).reshape(-1, self.nz))
         T = Z.shape[0]
-        noise = N.PF_NOISE_DEVICE if process_noise == "device" else N.PF_NOISE_NONE
+        noise = self._noise_mode(process_noise, replay, T)
         if tracker == "device":
             from . import trackers as TR
 
