@@ -568,14 +568,14 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, co
   c.xs = xs;
   c.xr = h->xr;
   c.lw = lw;
+  (void)d_means;  // (each wave centres on its own first particle: no shift needed from the outputs)
   c.flag = d_flags + s * R;
   c.lse = d_lse + s * R;
-  c.mean = d_means + s * R * h->nx;
   c.cov = d_covs + s * R * h->nx * h->nx;
   const dim3 blk(256);
   if (c.nb <= 3) {
     const dim3 grid((unsigned)c.nblk, (unsigned)R);
-    const size_t lds = 4 * (size_t)c.P * sizeof(double);
+    const size_t lds = 4 * (size_t)c.P * sizeof(double);  // per wave: M2 blocks | mean | W (== P for nb <= 3)
     if (h->esz == 4) {
       if (c.nb == 1) hipLaunchKernelGGL((k_cov_part<float, 1>), grid, blk, lds, h->stream, c);
       else if (c.nb == 2) hipLaunchKernelGGL((k_cov_part<float, 2>), grid, blk, lds, h->stream, c);
@@ -588,12 +588,12 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, co
   } else {
     if (c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
     const dim3 grid((unsigned)c.nblk, (unsigned)R, (unsigned)c.npairs);
-    const size_t lds = 4 * (size_t)(256 + 16 + 1) * sizeof(double);
+    const size_t lds = 4 * (size_t)cov_wave_slots<0>(1) * sizeof(double);
     if (h->esz == 4) hipLaunchKernelGGL((k_cov_part<float, 0>), grid, blk, lds, h->stream, c);
     else hipLaunchKernelGGL((k_cov_part<double, 0>), grid, blk, lds, h->stream, c);
   }
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_cov_sum, dim3((unsigned)((c.P + 15) / 16), (unsigned)R), dim3(256), 0, h->stream, c);
+  hipLaunchKernelGGL(k_cov_sum, dim3((unsigned)((c.npairs * 256 + 15) / 16), (unsigned)R), dim3(256), 0, h->stream, c);
   HIPCHK(hipGetLastError());
   return PF_OK;
 }

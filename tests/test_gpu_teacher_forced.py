@@ -10,10 +10,11 @@ the reference's outputs) is started from S_t, and both run step t with identical
 
 Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the step):
   particles after predict   |dx| <= 2e-6 x scale              (a few fp32 ulps of one step)
-  weights                   total-variation distance <= 1e-5 (MAT: 1e-4 - its 25 sensors at
-                            R = 0.01 I give log-likelihoods of O(1e2-1e3), whose fp32 rounding
-                            alone moves the normalised weights by O(1e-5))
-  Neff (pre-resample)       rel <= 1e-4
+  weights                   total-variation distance <= max(1e-5, 2^-20 (1 + E_w|log-lik|)): 16 fp32
+                            ulps of the log-weights' size (MAT's 25 sensors at R = 0.01 I give
+                            log-likelihoods of O(1e2-1e4), whose fp32 rounding alone moves the
+                            normalised weights by O(1e-4))
+  Neff                      rel <= max(1e-4, twice that bound)
   decision                  identical unless Neff is within 1e-3 N of 0.5 N
   ancestors                 every post-step slot is an exact copy of one predicted particle; where
                             that ancestor differs from the oracle's, the position lies within
@@ -22,8 +23,10 @@ Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the 
                             engine's ancestor: a near-tie of the two CDFs, nothing else
   posterior mean            <= 1e-5 x scale against the oracle's particles under the engine's
                             ancestors
-  posterior covariance      <= 2e-5 x max|cov| against np.cov of the same set (pf.py:266-267;
-                            nx > 4: the device loop's MFMA covariance, csrc/pf_cov.h)
+  posterior covariance      <= 2e-5 x max(max|cov|, (1e-6 scale)^2) against np.cov (pf.py:266-267)
+                            of the engine's own reported set (nx > 4: the device loop's MFMA
+                            covariance, csrc/pf_cov.h; the floor covers sets collapsed onto copies of
+                            one particle), and of the oracle's set within that + 4 |dx| / sigma
 The kernels covered: k_resident (config 2, N = 1e6), k_step_grp<float,40,10> (config 3, N = 1e5),
 k_step_grp<float,16,25> (config 4, 8 x 1e5: lane-local transition, v_rcp_f32 acoustic terms,
 rounds-aware tiles), k_step<float,1,1> over 64 x 1e6 (sv64) and k_step<double,1,1> (the fp64 line,
@@ -133,7 +136,7 @@ def test_step_grp_l96_config3():
 def test_step_grp_mat_config4():
     """k_step_grp<float,16,25>, BASELINE config 4's per-GPU batch (8 x 1e5, T = 100): lane-local
     transition, v_rcp_f32 acoustic terms, rounds-aware tiles."""
-    _, same = chain("mat", 100, n_bound=16, tol=dict(tol_tv=1e-4))
+    _, same = chain("mat", 100, n_bound=16)
     assert same
 
 
@@ -147,5 +150,5 @@ def test_step_sv64():
 def test_step_fp64_sv_config2():
     """k_step<double,1,1> (the fp64 line), config 2, T = 200: fp64 arithmetic, 32-bit Box-Muller."""
     chain("sv", 200, n_bound=10, precision="fp64",
-          tol=dict(tol_x=1e-12, tol_mean=1e-11, tol_neff=1e-10, tol_tv=1e-10, tol_cov=1e-10),
-          step_kw=dict(tie_floor=1e-12, exp_err=1e-15))
+          tol=dict(tol_x=1e-12, tol_mean=1e-11, tol_neff=1e-10, tol_tv=1e-10, tol_cov=1e-10, ulp=2.0 ** -48),
+          step_kw=dict(tie_floor=1e-12, exp_err=1e-15, cov_floor=1e-12))
