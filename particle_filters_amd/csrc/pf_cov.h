@@ -4,26 +4,27 @@
 // The reported state of step s is the post-resample particle set (uniform weights) when step s
 // resampled, else the predicted particles with their normalised weights w_i = e^(l_i - lse).
 // The step kernels cover nx <= 4 in their tile records; for larger states the record would need
-// nx(nx+1)/2 sums per tile, so the device loop computes it here instead, as the GEMM it is.
+// nx(nx+1)/2 sums per tile, so the device loop computes it here instead, as the GEMM it is:
 //
-// Numerics follow np.cov (centre, then multiply): each wave first takes its particles' weighted
-// mean c_w (about its first particle; a resampled set of copies gives exactly zero spread, as
-// np.cov does), then accumulates
-//   W_w = sum w_i,  S1_w = sum w_i (x_i - c_w),  S2_w = Y^T Y with Y[i][d] = sqrt(w_i) (x_id - c_wd)
-// (S2 by MFMA in 16x16 blocks over the upper block triangle: v_mfma_f32_16x16x4_f32 for the fp32
-// engine, fp32 partials over one wave's particles and fp64 from there on; v_mfma_f64_16x16x4 for
-// the fp64 engine; S1 / W by fp64 VALU), so m_w = c_w + S1_w / W_w and M2_w = S2_w - S1_w S1_w^T / W_w.
-// Waves, then blocks, then the whole set combine exactly (Chan et al.):
-//   W = sum W_b,  m = sum W_b m_b / W,  M2 = sum_b [M2_b + W_b (m_b - m)(m_b - m)^T],  cov = M2 / W.
-// Rows: the post-resample rows the gather wrote (StepParams::xr_out) or the predicted rows.  Fixed
-// reduction orders throughout (deterministic).
+//   Y[i][d] = sqrt(w_i) (x_id - c_d),  S2 = Y^T Y,  S1 = sum_i w_i (x_i - c),  W = sum_i w_i
+//   cov = S2 / W - (S1 / W)(S1 / W)^T
 //
-//   k_cov_part  grid (nblk, R, npz), 4 waves per block, wave w takes particles
-//               [(4 b + w) per_wave, +per_wave); NB > 0: every block pair of the upper triangle in one
-//               wave (nx <= 48); NB == 0: the block pair blockIdx.z (any nx).  -> block partials
-//               [pairs][256] M2_b | [nb][16] m_b | W_b
-//   k_cov_sum   grid (ceil(npairs 256 / 16), R), 16 entries x 16 lanes per workgroup: the lanes of an
-//               entry split the blocks; the last workgroup to finish (per replicate) writes cov.
+// with c the step's weighted (pre-resample) mean, already an output of the loop: the set is
+// centred before the products, so S1 / W is O(sampling noise) and nothing cancels.  Each workgroup
+// stages 256 particles' centred, weighted rows in LDS with coalesced loads (component-major, rows
+// padded so the MFMA operand reads are bank-conflict-free), then each of its 4 waves runs 16 MFMA
+// k-steps over 64 of them: S2 in 16x16 blocks over the upper block triangle (v_mfma_f32_16x16x4_f32
+// for the fp32 engine - fp32 sums over 64 particles, fp64 from there on - v_mfma_f64_16x16x4 for the
+// fp64 engine), S1 / W in fp64.  Rows: the post-resample rows the gather wrote (StepParams::xr_out)
+// or the predicted rows.  Fixed reduction orders throughout (deterministic).
+//
+//   k_cov_part  grid (ceil(N / 256), R, npz): NB > 0: every block pair of the upper triangle (nx <= 48);
+//               NB == 0: the block pair blockIdx.z (any nx).  -> block partials
+//               [pairs][256] S2 | [nb][16] S1 | W
+//               into a ring slot: the partials of up to Tc steps (Tc from a memory budget) wait
+//               there, so a step costs this one launch;
+//   k_cov_fin_sum / k_cov_fin_out  once per Tc steps (and at the end of the run): every entry's
+//               block sum in block order, then the chunk's covariances (symmetric).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,13 +38,12 @@ struct CovParams {
   const void* lw;       // [R][Npad] unnormalised log-weights of the step (Real)
   int64_t N, Npad;
   int nx, nb, npairs, P;   // blocks of 16 components, block pairs (upper triangle), partial size
-  int nblk, per_wave;      // blocks per replicate, particles per wave (multiple of 4)
+  int nblk;                // workgroups per replicate (256 particles each)
   const int32_t* flag;     // [R] resampled at this step
   const double* lse;       // [R] log normaliser of lw
-  double* part;            // [R][nblk][P]
-  double* tot;             // [R][P]
-  unsigned int* cnt;       // [R] workgroups of k_cov_sum done (the last one resets it)
-  double* cov;             // [R][nx][nx]
+  const double* mean;      // [R][nx] the step's weighted (pre-resample) mean: the centre
+  double* part;            // [R][nblk][P]: this step's ring slot
+  int diag;                // experiment knob (PF_COV_DIAG): 1 no staging loads, 2 no MFMA loop, 4 no output
 };
 
 __host__ __device__ inline int cov_pair_index(int bi, int bj, int nb) { return bi * nb - bi * (bi - 1) / 2 + (bj - bi); }
@@ -66,9 +66,7 @@ template <>
 struct CovMfma<float> {  // C/D: col = lane & 15, row = 4 (lane >> 4) + reg
   typedef cov_f4 acc_t;
   __device__ static acc_t zero() { return acc_t{0.f, 0.f, 0.f, 0.f}; }
-  __device__ static acc_t mma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32((float)a, (float)b, c, 0, 0, 0);
-  }
+  __device__ static acc_t mma(float a, float b, acc_t c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
   __device__ static int row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
 };
 template <>
@@ -79,24 +77,35 @@ struct CovMfma<double> {  // C/D: col = lane & 15, row = (lane >> 4) + 4 reg
   __device__ static int row(int lane, int reg) { return (lane >> 4) + 4 * reg; }
 };
 
-// LDS per workgroup: 4 waves x (NPW 256 M2 | NBL 16 mean | W) doubles
-template <int NB>
-__host__ __device__ constexpr int cov_wave_slots(int npw_runtime) {
-  return (NB > 0 ? NB * (NB + 1) / 2 : npw_runtime) * 256 + (NB > 0 ? NB : 2) * 16 + 1;
+constexpr int COV_BLK = 256;  // particles per workgroup (64 per wave: 16 MFMA k-steps)
+constexpr int COV_YS = COV_BLK + 4;  // LDS row stride (elements): lanes (col, kq) read 64 distinct banks
+
+// LDS bytes of k_cov_part: the staged rows (reused for the waves' sums) + sqrt weights
+template <typename Real, int NB>
+__host__ __device__ constexpr size_t cov_part_lds() {
+  constexpr int NBL = NB > 0 ? NB : 2, NPW = NB > 0 ? NB * (NB + 1) / 2 : 1;
+  constexpr size_t ys = (size_t)NBL * 16 * COV_YS * sizeof(Real);
+  constexpr size_t comb = 4 * ((size_t)NPW * 256 + NBL * 16 + 1) * sizeof(double);
+  return (ys > comb ? ys : comb) + (COV_BLK + NBL * 16) * sizeof(double);
 }
 
 // NB > 0: nb == NB, all NB (NB + 1) / 2 pairs per wave.  NB == 0: the pair blockIdx.z.
 template <typename Real, int NB>
 __global__ void __launch_bounds__(256) k_cov_part(CovParams p) {
   using MF = CovMfma<Real>;
-  constexpr int NBL = NB > 0 ? NB : 2;                 // row blocks a wave loads
-  constexpr int NPW = NB > 0 ? NB * (NB + 1) / 2 : 1;  // pairs a wave accumulates
-  constexpr int WS = cov_wave_slots<NB>(1);            // LDS doubles per wave
-  constexpr int OM = NPW * 256, OW = OM + NBL * 16;    // offsets of the means and W in a wave's slots
+  constexpr int NBL = NB > 0 ? NB : 2;                 // row blocks staged
+  constexpr int NPW = NB > 0 ? NB * (NB + 1) / 2 : 1;  // pairs per wave
+  constexpr int WS = NPW * 256 + NBL * 16 + 1;         // one wave's sums (doubles)
   extern __shared__ __attribute__((aligned(16))) double cs[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+  constexpr size_t YB = (size_t)NBL * 16 * COV_YS * sizeof(Real);
+  constexpr size_t CB = 4 * (size_t)WS * sizeof(double);
+  Real* ys = (Real*)cs;                                               // [NBL * 16][COV_YS]
+  double* sws = cs + (YB > CB ? YB : CB) / sizeof(double);            // [256] sqrt weights
+  double* cl = sws + COV_BLK;                                         // [NBL * 16] the centre
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, col = lane & 15, kq = lane >> 4;
   const int b = blockIdx.x, r = blockIdx.y;
-  int blk[NBL];  // the row blocks this wave loads
+  if (p.diag & 32) return;
+  int blk[NBL];
   int pair0 = 0;
   if constexpr (NB > 0) {
 #pragma unroll
@@ -107,62 +116,59 @@ __global__ void __launch_bounds__(256) k_cov_part(CovParams p) {
   }
   const bool res = p.flag[r] != 0;
   const Real* X = (const Real*)(res ? p.xr : p.xs) + (int64_t)r * p.nx * p.Npad;
-  const Real* L = (const Real*)p.lw + (int64_t)r * p.Npad;
-  const double lse = p.lse[r], swu = sqrt(1.0 / (double)p.N);  // uniform weights: sqrt(1/N)
-  const int64_t i0 = ((int64_t)b * 4 + w) * p.per_wave;
-  const int64_t i1 = min(i0 + (int64_t)p.per_wave, p.N);
-  int dd[NBL];
-  double cd[NBL];  // the wave's centre: its weighted mean (pass 1, about its first particle)
-#pragma unroll
-  for (int k = 0; k < NBL; ++k) {
-    dd[k] = blk[k] * 16 + col;
-    cd[k] = (i0 < i1 && dd[k] < p.nx) ? (double)X[(int64_t)dd[k] * p.Npad + i0] : 0.0;
+  const double* c = p.mean + (int64_t)r * p.nx;
+  const int64_t base = (int64_t)b * COV_BLK;
+  const bool live = base + t < p.N;
+  if (t < NBL * 16) {  // the centre through LDS: one vector load instead of a serial scalar-load chain
+    const int d = blk[t >> 4] * 16 + (t & 15);
+    cl[t] = d < p.nx ? c[d] : 0.0;
   }
-  auto weight_root = [&](int64_t i) -> double {  // sqrt(w_i) of this lane's particle (0 past the range)
-    if (i >= i1) return 0.0;
-    if (res) return swu;
-    const Real l = L[i];
-    return (l > -INFINITY) ? sqrt(exp((double)l - lse)) : 0.0;
-  };
-  {
-    double m1[NBL], w1 = 0.0;
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) m1[k] = 0.0;
-    for (int64_t ib = i0; ib < i1; ib += 4) {
-      const int64_t i = ib + kq;
-      const double sw = weight_root(i);
-      const double wi = sw * sw;
-      w1 += wi;
-#pragma unroll
-      for (int k = 0; k < NBL; ++k)
-        if (i < i1 && dd[k] < p.nx) m1[k] += wi * ((double)X[(int64_t)dd[k] * p.Npad + i] - cd[k]);
-    }
-    w1 += __shfl_xor(w1, 16);
-    w1 += __shfl_xor(w1, 32);
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) {
-      m1[k] += __shfl_xor(m1[k], 16);
-      m1[k] += __shfl_xor(m1[k], 32);
-      if (w1 > 0.0) cd[k] += m1[k] / w1;
+  // ---- stage: thread t = particle base + t (coalesced rows), sqrt(w) and the centred rows ----
+  double sw = 0.0;
+  if (live) {
+    if (res) {
+      sw = sqrt(1.0 / (double)p.N);
+    } else {
+      const Real l = ((const Real*)p.lw)[(int64_t)r * p.Npad + base + t];
+      sw = (l > -INFINITY) ? sqrt(exp((double)l - p.lse[r])) : 0.0;
     }
   }
+  sws[t] = sw;
+  // unconditional loads from clamped addresses (all issued before the first use), masked after
+  const int64_t col_i = live ? base + t : 0;
+  __syncthreads();  // cl
+  Real xv[NBL][16];
+#pragma unroll
+  for (int k = 0; k < NBL; ++k)
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) xv[k][cc] = X[(int64_t)min(blk[k] * 16 + cc, p.nx - 1) * p.Npad + col_i];
+#pragma unroll
+  for (int k = 0; k < NBL; ++k)
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      const int d = blk[k] * 16 + cc;
+      const double v = (d < p.nx && !(p.diag & 1)) ? sw * ((double)xv[k][cc] - cl[k * 16 + cc]) : 0.0;
+      ys[(k * 16 + cc) * COV_YS + t] = (Real)v;
+    }
+  __syncthreads();
+  // ---- this wave's 64 particles: 16 MFMA k-steps per pair, S1 / W in fp64 ----
   typename MF::acc_t acc[NPW];
 #pragma unroll
   for (int q = 0; q < NPW; ++q) acc[q] = MF::zero();
   double s1[NBL], wsum = 0.0;
 #pragma unroll
   for (int k = 0; k < NBL; ++k) s1[k] = 0.0;
-  for (int64_t ib = i0; ib < i1; ib += 4) {
-    const int64_t i = ib + kq;  // this lane's particle (k index of the MFMA)
-    const double sw = weight_root(i);
-    double y[NBL];
+#pragma unroll 4
+  for (int st = 0; st < ((p.diag & 2) ? 0 : 16); ++st) {
+    const int i = w * 64 + 4 * st + kq;
+    const double swi = sws[i];
+    Real y[NBL];
 #pragma unroll
     for (int k = 0; k < NBL; ++k) {
-      const bool in = i < i1 && dd[k] < p.nx;
-      y[k] = in ? sw * ((double)X[(int64_t)dd[k] * p.Npad + i] - cd[k]) : 0.0;
-      s1[k] += sw * y[k];
+      y[k] = ys[(k * 16 + col) * COV_YS + i];
+      s1[k] += swi * (double)y[k];
     }
-    if (col == 0) wsum += sw * sw;
+    if (col == 0) wsum += swi * swi;
     if constexpr (NB > 0) {
       int q = 0;
 #pragma unroll
@@ -173,7 +179,6 @@ __global__ void __launch_bounds__(256) k_cov_part(CovParams p) {
       acc[0] = MF::mma(y[0], y[1], acc[0]);
     }
   }
-  // S1 / W over the four k lanes of each column
 #pragma unroll
   for (int k = 0; k < NBL; ++k) {
     s1[k] += __shfl_xor(s1[k], 16);
@@ -181,134 +186,71 @@ __global__ void __launch_bounds__(256) k_cov_part(CovParams p) {
   }
   wsum += __shfl_xor(wsum, 16);
   wsum += __shfl_xor(wsum, 32);
-  wsum = __shfl(wsum, 0);
-  // this wave's mean and S1 (LDS, for the rows of its MFMA tiles), then M2_w = S2 - S1 S1^T / W
+  __syncthreads();  // the staged rows are consumed: their LDS now takes the waves' sums
   double* mine = cs + (int64_t)w * WS;
+#pragma unroll
+  for (int q = 0; q < NPW; ++q)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mine[q * 256 + MF::row(lane, g) * 16 + col] = (double)acc[q][g];
   if (kq == 0) {
 #pragma unroll
-    for (int k = 0; k < NBL; ++k) {
-      mine[OM + k * 16 + col] = s1[k];  // S1 for now, the mean below
-    }
-    if (col == 0) mine[OW] = wsum;
+    for (int k = 0; k < NBL; ++k) mine[NPW * 256 + k * 16 + col] = s1[k];
+    if (col == 0) mine[NPW * 256 + NBL * 16] = wsum;
   }
   __syncthreads();
-  const double iw = wsum > 0.0 ? 1.0 / wsum : 0.0;
-#pragma unroll
-  for (int q = 0; q < NPW; ++q) {
-    int a = 0, c2 = 1;  // the wave-local block indices of pair q
-    if constexpr (NB > 0) {
-      int bi = 0, bj = 0;
-      cov_pair_blocks(q, NB, &bi, &bj);
-      a = bi;
-      c2 = bj;
-    } else {
-      a = 0;
-      c2 = 1;
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int rw = MF::row(lane, g);
-      const double m2 = (double)acc[q][g] - mine[OM + a * 16 + rw] * mine[OM + c2 * 16 + col] * iw;
-      mine[q * 256 + rw * 16 + col] = m2;
-    }
-  }
-  __syncthreads();
-  if (kq == 0) {
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) mine[OM + k * 16 + col] = cd[k] + mine[OM + k * 16 + col] * iw;  // m_w
-  }
-  __syncthreads();
-  // the block's 4 waves combined (Chan): W_b, m_b, M2_b
   double* out = p.part + ((int64_t)r * p.nblk + b) * p.P;
-  double Wb = 0.0;
-  for (int v = 0; v < 4; ++v) Wb += cs[v * WS + OW];
-  const double iWb = Wb > 0.0 ? 1.0 / Wb : 0.0;
-  __shared__ double mb[NBL * 16];
-  for (int e = threadIdx.x; e < NBL * 16; e += 256) {
-    double s = 0.0;
-    for (int v = 0; v < 4; ++v) s += cs[v * WS + OW] * cs[v * WS + OM + e];
-    mb[e] = s * iWb;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < NPW * 256; e += 256) {
-    const int q = e >> 8, rw = (e >> 4) & 15, cl = e & 15;
-    int a = 0, c2 = 1;
-    if constexpr (NB > 0) cov_pair_blocks(q, NB, &a, &c2);
-    double s = 0.0;
-    for (int v = 0; v < 4; ++v) {
-      const double* wv = cs + v * WS;
-      const double da = wv[OM + a * 16 + rw] - mb[a * 16 + rw], dc = wv[OM + c2 * 16 + cl] - mb[c2 * 16 + cl];
-      s += wv[e] + wv[OW] * da * dc;
+  for (int e = t; e < ((p.diag & 4) ? 0 : WS); e += 256) {
+    const double v = ((cs[e] + cs[WS + e]) + cs[2 * WS + e]) + cs[3 * WS + e];
+    if constexpr (NB > 0) {
+      out[e] = v;
+    } else {  // this pair's block, its S1 block (diagonal pairs) and W (pair 0)
+      if (e < 256) out[pair0 * 256 + e] = v;
+      else if (e < 256 + 16) { if (blk[0] == blk[1]) out[p.npairs * 256 + blk[0] * 16 + (e - 256)] = v; }
+      else if (e == 256 + 32 && pair0 == 0) out[p.npairs * 256 + p.nb * 16] = v;
     }
-    out[(NB > 0 ? 0 : pair0 * 256) + e] = s;
   }
-  const int nbl = NB > 0 ? NB : 1;  // mean blocks this workgroup owns (diagonal pairs only for NB == 0)
-  if (NB > 0 || blk[0] == blk[1]) {
-    for (int e = threadIdx.x; e < nbl * 16; e += 256) out[p.npairs * 256 + blk[0] * 16 * (NB > 0 ? 0 : 1) + e] = mb[e];
-  }
-  if (threadIdx.x == 0 && (NB > 0 || pair0 == 0)) out[p.npairs * 256 + p.nb * 16] = Wb;
 }
 
-// M2 entries over the blocks (Chan), 16 lanes per entry splitting the blocks; the last workgroup
-// to finish per replicate writes cov = M2 / W (symmetric).
-__global__ void __launch_bounds__(256) k_cov_sum(CovParams p) {
-  const int r = blockIdx.y, t = threadIdx.x, sub = t & 15;
-  const int e = blockIdx.x * 16 + (t >> 4);  // M2 slot: pair e >> 8, row (e >> 4) & 15, col e & 15
-  const double* base = p.part + (int64_t)r * p.nblk * p.P;
-  const int OM = p.npairs * 256, OW = OM + p.nb * 16;
-  double* T = p.tot + (int64_t)r * p.P;
-  if (e < p.npairs * 256) {
-    int bi = 0, bj = 0;
-    cov_pair_blocks(e >> 8, p.nb, &bi, &bj);
-    const int d = bi * 16 + ((e >> 4) & 15), f = bj * 16 + (e & 15);
-    double W = 0.0, md = 0.0, mf = 0.0;
-    for (int k = sub; k < p.nblk; k += 16) {
-      const double* q = base + (int64_t)k * p.P;
-      const double wk = q[OW];
-      W += wk;
-      md += wk * q[OM + d];
-      mf += wk * q[OM + f];
-    }
+// The blocks' partials of n consecutive steps (a chunk of the ring the k_cov_part launches fill)
+// summed per entry in block order - one lane per entry, 16 independent loads in flight - then
+// cov = S2 / W - (S1 / W)(S1 / W)^T per step, exactly symmetric.  Two launches per chunk.
+struct CovFin {
+  const double* part;  // [n][R][nblk][P]
+  double* tot;         // [n][R][P]
+  double* cov;         // [n][R][nx][nx]: the chunk's first step
+  int R, nblk, P, nx, nb, npairs;
+};
+
+// grid (ceil(P / 256), n R), 256 threads
+__global__ void __launch_bounds__(256) k_cov_fin_sum(CovFin f) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int64_t jr = blockIdx.y;  // step-in-chunk * R + replicate
+  if (e >= f.P) return;
+  const double* src = f.part + jr * f.nblk * f.P + e;
+  double s = 0.0;
+  for (int k0 = 0; k0 < f.nblk; k0 += 16) {
+    double v[16];
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      W += __shfl_xor(W, o);
-      md += __shfl_xor(md, o);
-      mf += __shfl_xor(mf, o);
-    }
-    const double iW = W > 0.0 ? 1.0 / W : 0.0;
-    md *= iW;
-    mf *= iW;
-    double s = 0.0;
-    for (int k = sub; k < p.nblk; k += 16) {
-      const double* q = base + (int64_t)k * p.P;
-      s += q[e] + q[OW] * (q[OM + d] - md) * (q[OM + f] - mf);
-    }
+    for (int k = 0; k < 16; ++k) v[k] = k0 + k < f.nblk ? src[(int64_t)(k0 + k) * f.P] : 0.0;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (sub == 0) {
-      T[e] = s;
-      if (e == 0) T[OW] = W;
-    }
+    for (int k = 0; k < 16; ++k) s += v[k];
   }
-  __threadfence();
-  __shared__ int last;
-  __syncthreads();
-  if (t == 0) last = atomicAdd(p.cnt + r, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // the other workgroups' sums: device-coherent loads (never a line this CU's L1 may hold)
-  auto ld = [](const double* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  const double W = ld(T + OW);
+  f.tot[jr * f.P + e] = s;
+}
+
+// grid (ceil(nx^2 / 256), n R), 256 threads
+__global__ void __launch_bounds__(256) k_cov_fin_out(CovFin f) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  const int64_t jr = blockIdx.y;
+  if (g >= f.nx * f.nx) return;
+  const double* T = f.tot + jr * f.P;
+  const int OM = f.npairs * 256;
+  const double W = T[OM + f.nb * 16];
   const double iW = W > 0.0 ? 1.0 / W : 0.0;
-  double* cov = p.cov + (int64_t)r * p.nx * p.nx;
-  for (int g = t; g < p.nx * p.nx; g += 256) {
-    const int d0 = g / p.nx, f0 = g % p.nx;
-    const int d = min(d0, f0), f = max(d0, f0);  // the upper-triangle entry for both: exactly symmetric
-    const double m2 = ld(T + cov_pair_index(d >> 4, f >> 4, p.nb) * 256 + (d & 15) * 16 + (f & 15));
-    cov[g] = m2 * iW;
-  }
-  if (t == 0) p.cnt[r] = 0u;
+  const int d0 = g / f.nx, f0 = g % f.nx;
+  const int d = min(d0, f0), c = max(d0, f0);  // the upper-triangle entry for both: exactly symmetric
+  const double s2 = T[cov_pair_index(d >> 4, c >> 4, f.nb) * 256 + (d & 15) * 16 + (c & 15)];
+  f.cov[jr * f.nx * f.nx + g] = s2 * iW - (T[OM + d] * iW) * (T[OM + c] * iW);
 }
 
 }  // namespace pf

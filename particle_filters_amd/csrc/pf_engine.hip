@@ -230,7 +230,9 @@ struct pf_handle {
   void* xr = nullptr;
   double* cov_part = nullptr;
   double* cov_tot = nullptr;
-  unsigned int* cov_cnt = nullptr;
+  int cov_tc = 0;       // ring slots (steps) of partials
+  int64_t cov_s0 = 0;   // first step of the pending chunk
+  int cov_pending = 0;  // steps in the ring
   CovParams covp{};
   // live kernel timing (pf_set_timing): events recorded on the handle's stream right
   // before the first and after the last filter kernel of each pf_run_device
@@ -543,58 +545,92 @@ pf_status ensure_cov(pf_handle* h) {
   c.nb = (h->nx + 15) / 16;
   c.npairs = c.nb * (c.nb + 1) / 2;
   c.P = c.npairs * 256 + c.nb * 16 + 1;
-  const int64_t waves_rep = c.nb <= 3 ? std::max<int64_t>(4, 2048 / h->R) : 4;
-  int64_t per = (h->N + waves_rep - 1) / waves_rep;
-  per = std::max<int64_t>(4, (per + 3) / 4 * 4);
-  c.per_wave = (int)per;
-  c.nblk = (int)((h->N + 4 * per - 1) / (4 * per));
+  c.nblk = (int)((h->N + COV_BLK - 1) / COV_BLK);
   HIPCHK(hipMalloc(&h->xr, (size_t)h->R * h->nx * h->Npad * h->esz));
-  HIPCHK(hipMalloc((void**)&h->cov_part, (size_t)h->R * c.nblk * c.P * sizeof(double)));
-  HIPCHK(hipMalloc((void**)&h->cov_tot, (size_t)h->R * c.P * sizeof(double)));
-  HIPCHK(hipMalloc((void**)&h->cov_cnt, (size_t)h->R * sizeof(unsigned int)));
-  HIPCHK(hipMemset(h->cov_cnt, 0, (size_t)h->R * sizeof(unsigned int)));
-  c.part = h->cov_part;
-  c.tot = h->cov_tot;
-  c.cnt = h->cov_cnt;
+  const size_t slot = (size_t)h->R * c.nblk * c.P * sizeof(double);
+  h->cov_tc = (int)std::max<size_t>(1, std::min<size_t>(32, ((size_t)256 << 20) / slot));  // <= 256 MiB of ring
+  HIPCHK(hipMalloc((void**)&h->cov_part, (size_t)h->cov_tc * slot));
+  HIPCHK(hipMalloc((void**)&h->cov_tot, (size_t)h->cov_tc * h->R * c.P * sizeof(double)));
+  h->cov_pending = 0;
+  c.diag = std::getenv("PF_COV_DIAG") ? std::atoi(std::getenv("PF_COV_DIAG")) : 0;
+  if (c.nb > 3 && c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
+  static bool attr_done = false;  // dynamic LDS above 64 KiB (fp64 rows, nb = 3)
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)cov_part_lds<double, 3>());
+    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)cov_part_lds<double, 2>());
+    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)cov_part_lds<double, 0>());
+    attr_done = true;
+  }
+  return PF_OK;
+}
+
+template <typename Real, int NB>
+void launch_cov_part(dim3 grid, const CovParams& c, hipStream_t s) {
+  const size_t lds = cov_part_lds<Real, NB>();
+  hipLaunchKernelGGL((k_cov_part<Real, NB>), grid, dim3(256), lds, s, c);
+}
+
+// The pending chunk of the ring -> d_covs[s0 .. s0 + pending)
+pf_status flush_cov(pf_handle* h, double* d_covs) {
+  if (h->cov_pending == 0) return PF_OK;
+  const CovParams& c = h->covp;
+  CovFin f;
+  f.part = h->cov_part;
+  f.tot = h->cov_tot;
+  f.cov = d_covs + h->cov_s0 * h->R * h->nx * h->nx;
+  f.R = h->R;
+  f.nblk = c.nblk;
+  f.P = c.P;
+  f.nx = h->nx;
+  f.nb = c.nb;
+  f.npairs = c.npairs;
+  const unsigned nr = (unsigned)(h->cov_pending * h->R);
+  hipLaunchKernelGGL(k_cov_fin_sum, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_cov_fin_out, dim3((unsigned)((h->nx * h->nx + 255) / 256), nr), dim3(256), 0, h->stream, f);
+  HIPCHK(hipGetLastError());
+  h->cov_pending = 0;
   return PF_OK;
 }
 
 // Covariance of step s (its predicted rows xs / log-weights lw; the post-resample rows in h->xr,
-// written by the gather that followed) into d_covs[s], from the step's outputs (flag, lse, mean).
+// written by the gather that followed) from the step's outputs (flag, lse, mean): its block
+// partials into the ring; d_covs[s] when the chunk is flushed (full, or the end of the run).
 pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, const double* d_means,
                      const int32_t* d_flags, const double* d_lse, double* d_covs) {
   CovParams c = h->covp;
   const int R = h->R;
+  if (h->cov_pending == 0) h->cov_s0 = s;
+  if (s != h->cov_s0 + h->cov_pending) return fail(PF_E_ARG, "device-loop covariance: steps out of order");
+  c.part = h->cov_part + (size_t)h->cov_pending * R * c.nblk * c.P;
   c.xs = xs;
   c.xr = h->xr;
   c.lw = lw;
-  (void)d_means;  // (each wave centres on its own first particle: no shift needed from the outputs)
   c.flag = d_flags + s * R;
   c.lse = d_lse + s * R;
-  c.cov = d_covs + s * R * h->nx * h->nx;
-  const dim3 blk(256);
+  c.mean = d_means + s * R * h->nx;
+  const bool f32 = h->esz == 4;
   if (c.nb <= 3) {
     const dim3 grid((unsigned)c.nblk, (unsigned)R);
-    const size_t lds = 4 * (size_t)c.P * sizeof(double);  // per wave: M2 blocks | mean | W (== P for nb <= 3)
-    if (h->esz == 4) {
-      if (c.nb == 1) hipLaunchKernelGGL((k_cov_part<float, 1>), grid, blk, lds, h->stream, c);
-      else if (c.nb == 2) hipLaunchKernelGGL((k_cov_part<float, 2>), grid, blk, lds, h->stream, c);
-      else hipLaunchKernelGGL((k_cov_part<float, 3>), grid, blk, lds, h->stream, c);
+    if (f32) {
+      if (c.nb == 1) launch_cov_part<float, 1>(grid, c, h->stream);
+      else if (c.nb == 2) launch_cov_part<float, 2>(grid, c, h->stream);
+      else launch_cov_part<float, 3>(grid, c, h->stream);
     } else {
-      if (c.nb == 1) hipLaunchKernelGGL((k_cov_part<double, 1>), grid, blk, lds, h->stream, c);
-      else if (c.nb == 2) hipLaunchKernelGGL((k_cov_part<double, 2>), grid, blk, lds, h->stream, c);
-      else hipLaunchKernelGGL((k_cov_part<double, 3>), grid, blk, lds, h->stream, c);
+      if (c.nb == 1) launch_cov_part<double, 1>(grid, c, h->stream);
+      else if (c.nb == 2) launch_cov_part<double, 2>(grid, c, h->stream);
+      else launch_cov_part<double, 3>(grid, c, h->stream);
     }
   } else {
-    if (c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
     const dim3 grid((unsigned)c.nblk, (unsigned)R, (unsigned)c.npairs);
-    const size_t lds = 4 * (size_t)cov_wave_slots<0>(1) * sizeof(double);
-    if (h->esz == 4) hipLaunchKernelGGL((k_cov_part<float, 0>), grid, blk, lds, h->stream, c);
-    else hipLaunchKernelGGL((k_cov_part<double, 0>), grid, blk, lds, h->stream, c);
+    if (f32) launch_cov_part<float, 0>(grid, c, h->stream);
+    else launch_cov_part<double, 0>(grid, c, h->stream);
   }
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_cov_sum, dim3((unsigned)((c.npairs * 256 + 15) / 16), (unsigned)R), dim3(256), 0, h->stream, c);
-  HIPCHK(hipGetLastError());
+  if (++h->cov_pending == h->cov_tc) return flush_cov(h, d_covs);
   return PF_OK;
 }
 
@@ -1036,8 +1072,7 @@ void pf_destroy(pf_handle* h) {
   for (double* q : h->lcum)
     if (q) (void)hipFree(q);
   for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
-                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->cov_part, (void*)h->cov_tot,
-                  (void*)h->cov_cnt})
+                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->cov_part, (void*)h->cov_tot})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1255,6 +1290,7 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   if (cov_loop) {
     pf_status st = ensure_cov(h);
     if (st) return st;
+    h->cov_pending = 0;
     p.xr_out = h->xr;
   }
   p.o_neff = d_neff;
@@ -1308,6 +1344,8 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
   if (st) return st;
   if (cov_loop) {
     st = launch_cov(h, xs_last, lw_last, T - 1, d_means, d_flags, d_lse, d_covs);
+    if (st) return st;
+    st = flush_cov(h, d_covs);
     if (st) return st;
   }
   p.out_step = -1;

@@ -72,8 +72,9 @@ def check_vs_oracle(g, h, ssm, Q, R, Z, *, N, n_rep=1, seed=5, mean0, cov0, meth
 
 
 def test_l96_d40_compiled_step():
+    """T = 40 > the 32-step ring of block partials: two chunk flushes."""
     wl = bench.WORKLOADS["l96"]()
-    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(15, 0)
+    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(40, 0)
     check_vs_oracle(g, h, wl.oracle_ssm(), np.asarray(Q, float), np.asarray(R, float), np.asarray(Z, float), N=2000,
                     mean0=mean0, cov0=cov0)
 
