@@ -35,6 +35,9 @@ constexpr int FPPB = 256;                      // max particles per workgroup (N
 constexpr int FMC = 64;                        // particles per moment chunk (staged in LDS)
 constexpr unsigned FSPIN = 1u << 24;           // barrier spin limit (then the launch fails)
 constexpr int FNST = 4;                        // source CDF slices staged in LDS per moment chunk
+#ifndef PF_LEDH_LDS
+#define PF_LEDH_LDS 1                          // parameters and composed flow staged in LDS (P1)
+#endif
 
 // diagnostic phase stamps (PF_STAMPS builds only): s_memrealtime (100 MHz) per workgroup
 #ifdef PF_STAMPS
@@ -126,6 +129,38 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   LF_STAMP(0);
 
   // ---- P1: flow --------------------------------------------------------------------
+  // The parameter block and the composed flow are read by every lane group many times over
+  // (H, D, QL, ... at lane-dependent offsets): staged once per workgroup in LDS, so the
+  // per-particle chain waits on LDS instead of L2 round trips at one wave per SIMD.
+#if PF_LEDH_LDS
+  using L = Lay<NX, NZ>;
+  using TL = TLay<NX, NZ>;
+  __shared__ double pms[L::SIZE];
+  __shared__ double afs[TL::AFF_SIZE];
+  {
+    const bool qd = p.f.q_diag != 0;
+    auto need = [&](int k) {
+      if (k < L::EX) return TK != PF_TRANS_L96;             // A (linear g)
+      if (k < L::AC) return true;                           // F, dt, H, c
+      if (k < L::LQ) return false;                          // acoustic geometry (not a linear h)
+      if (k < L::R) {                                       // chol(Q), Q^{-1}: the diagonal when diagonal
+        const int e = (k - L::LQ) % (NX * NX);
+        return !qd || (e / NX == e % NX);
+      }
+      return k >= L::RI;                                    // R^{-1}
+    };
+    for (int k = t; k < L::SIZE; k += FB)
+      if (need(k)) pms[k] = p.f.Pm[k];
+    const double* __restrict__ afg = p.f.table + TL::aff(p.f.L);
+    for (int k = t; k < TL::AFF_SIZE; k += FB) afs[k] = afg[k];
+    __syncthreads();
+  }
+  const double* Pm_f = pms;
+  const double* af_f = afs;
+#else
+  const double* Pm_f = p.f.Pm;
+  const double* af_f = p.f.table + TLay<NX, NZ>::aff(p.f.L);
+#endif
   double m = -INFINITY;
   {
     const int q = t % GL, slot = t / GL, base = lane - q;
@@ -133,7 +168,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       const int j = c0 + slot;
       const bool live = j < n;
       // whole lane groups stay together; dead groups run particle i0 (results discarded)
-      const double l = flow_affine_particle<NX, NZ, TK, true>(p.f, live ? i0 + j : i0, q, base);
+      const double l = flow_affine_particle<NX, NZ, TK, true>(p.f, Pm_f, af_f, live ? i0 + j : i0, q, base);
       if (live && q == 0) lws[j] = l;
       if (live) m = fmax(m, l);
     }

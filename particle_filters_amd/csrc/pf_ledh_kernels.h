@@ -540,10 +540,10 @@ __device__ __forceinline__ double group_sum(double v) {
 // eta0 = g(x_{k-1}, u) + v of particle i over a lane group (ledh.py:104-115): gx = g(x) and v
 // (PER components per lane, lane q of the group holds components q*PER ..)
 template <int NX, int NZ, int TK>
-__device__ __forceinline__ void group_prior(const FlowParams& p, int64_t i, int q, int base, double* gx, double* v) {
+__device__ __forceinline__ void group_prior(const FlowParams& p, const double* __restrict__ Pm, int64_t i, int q,
+                                            int base, double* gx, double* v) {
   using L = Lay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  const double* __restrict__ Pm = p.Pm;
   double x[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -624,11 +624,10 @@ __device__ __forceinline__ void group_prior(const FlowParams& p, int64_t i, int 
 // log N(eta; g(x), Q) - log N(eta0; g(x), Q) up to the cancelling constant (ledh.py:186-190),
 // dd = eta - g(x), v = eta0 - g(x); summed over the lane group
 template <int NX, int NZ>
-__device__ __forceinline__ double group_trans_part(const FlowParams& p, int q, int base, const double* dd,
-                                                   const double* v) {
+__device__ __forceinline__ double group_trans_part(const FlowParams& p, const double* __restrict__ Pm, int q, int base,
+                                                   const double* dd, const double* v) {
   using L = Lay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  const double* __restrict__ Pm = p.Pm;
   double part = 0.0;
   if (p.q_diag) {
 #pragma unroll
@@ -665,15 +664,16 @@ __device__ __forceinline__ double wt_load(const double* p) {
 
 // The affine flow of particle i by its lane group (lane q of GL): writes eta_L to x_out
 // (write-through when WT) and returns the unnormalised log weight (valid in every lane of the group).
+// Pm: the parameter block (Lay), af: the composed flow (TLay::aff) - p.Pm / p.table in HBM, or
+// copies staged in LDS (k_ledh_fused).
 template <int NX, int NZ, int TK, bool WT = false>
-__device__ __forceinline__ double flow_affine_particle(const FlowParams& p, int64_t i, int q, int base) {
+__device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
+                                                      const double* __restrict__ af, int64_t i, int q, int base) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  const double* __restrict__ Pm = p.Pm;
-  const double* __restrict__ af = p.table + T::aff(p.L);
   double gx[PER], v[PER];
-  group_prior<NX, NZ, TK>(p, i, q, base, gx, v);
+  group_prior<NX, NZ, TK>(p, Pm, i, q, base, gx, v);
   // ---- eta0, y0 = H eta0 (group all-reduce), the composed flow ----------------------
   double e0[PER];
 #pragma unroll
@@ -705,7 +705,7 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, int6
     }
   }
   // ---- log weight (ledh.py:186-190) -----------------------------------------------
-  const double part = group_trans_part<NX, NZ>(p, q, base, dd, v);
+  const double part = group_trans_part<NX, NZ>(p, Pm, q, base, dd, v);
   double ez[NZ];
 #pragma unroll
   for (int k = 0; k < NZ; ++k) {
@@ -726,7 +726,7 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
   if (i >= p.N) return;  // whole groups leave together
   const int q = (int)(tid % GL);
   const int base = (threadIdx.x & 63) - q;
-  const double l = flow_affine_particle<NX, NZ, TK>(p, i, q, base);
+  const double l = flow_affine_particle<NX, NZ, TK>(p, p.Pm, p.table + TLay<NX, NZ>::aff(p.L), i, q, base);
   if (q == 0) p.lw[i] = l;
 }
 
