@@ -639,7 +639,9 @@ def main():
 
     # the series also covers the CPU baselines' samples (they start at the timed window)
     cpu_need = 0 if (rank != 0 or args.no_cpu_baseline) else wl.cpu_steps * 5
-    T_data = W + max(K, cpu_need)
+    # nx > 4 with the covariance: a second window of K steps times the step kernels alone
+    split_cov = (not args.no_cov) and wl.nx > 4
+    T_data = W + max(K * (2 if split_cov else 1), cpu_need)
     g, h, Q, R, Zall, truth_all, mean0, cov0 = wl.build(T_data, rank)
     nx, Rl, Np = wl.nx, wl.replicates, wl.n_particles
     strong = args.replicates_total is not None
@@ -759,15 +761,34 @@ def main():
         allm = np.transpose(ot[0].cpu().numpy(), (1, 0, 2))
     rmse = [float(np.sqrt(np.mean((allm[r] - truth) ** 2))) for r in range(allm.shape[0])]
     local_flags = ot[2].cpu().numpy()  # [K][R] this rank's resample decisions
+    means_rep0 = ot[0][:, 0].cpu().numpy()  # replicate 0's means (rmse_vs_ref)
     resample_rate = float(local_flags.mean())
+
+    # nx > 4: the run's device time covers the step kernels AND the covariance kernels (pf_cov.h).
+    # The roofline is the dominant kernel's (the step kernel): time the next K steps (the data's
+    # continuation, same state) without the covariance; the difference is the covariance's cost.
+    cov_ms = None
+    if split_cov:
+        ox = outs(K)  # the timed window's outputs were read above; the storage is reused
+        ax = list(run_args(dz(Zall[W + K:W + 2 * K]), K, ox))
+        ax[6] = None  # no covariance
+        NV.check(lib.pf_run_device(*ax), "pf_run_device (step kernels only)")
+        NV.check(lib.pf_synchronize(pf.handle), "step-kernel window")
+        ms2 = NV.C.c_float()
+        NV.check(lib.pf_last_run_ms(pf.handle, NV.C.byref(ms2)), "pf_last_run_ms")
+        cov_ms = device_ms - float(ms2.value)
+        local_flags2 = ox[2].cpu().numpy()
+        device_ms_step, flags_step = float(ms2.value), local_flags2
+    else:
+        device_ms_step, flags_step = device_ms, None
 
     # live roofline of the dominant kernel: device time of the timed run
     resident = bool(lib.pf_last_run_resident(pf.handle))
-    step_s = device_ms * 1e-3 / K
+    step_s = device_ms_step * 1e-3 / K
     esz = 4.0 if args.precision == "fp32" else 8.0
     base_b, res_b = 2 * esz * nx + 2 * esz, 2 * esz * nx + 12.0  # SURVEY.md 8(d) at the storage width
-    alg_bytes_run = Np * (K * Rl * base_b + float(local_flags.sum()) * res_b)
-    achieved = alg_bytes_run / (device_ms * 1e-3) / 1e9
+    alg_bytes_run = Np * (K * Rl * base_b + float((local_flags if flags_step is None else flags_step).sum()) * res_b)
+    achieved = alg_bytes_run / (device_ms_step * 1e-3) / 1e9
     dyn = lib.pf_kernel_path(pf.handle) == NV.PF_PATH_RUNTIME
     # large states: group kernel; shapes outside the compiled list: the runtime-shape kernel
     kname = "k_resident" if resident else ("k_dyn_step" if dyn else ("k_step_grp" if nx >= 16 else "k_step"))
@@ -812,7 +833,7 @@ def main():
         ref = None
         if not args.no_ref:
             try:
-                ref = rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, ot[0][:, 0].cpu().numpy(),
+                ref = rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, means_rep0,
                                   local_flags[:, 0], args.precision)
                 if wl.nx > 1 and len(rmse) > 1 and "abs_diff" in ref:
                     # large states: after the first fp32-vs-fp64 decision flip the replicate-0
@@ -870,7 +891,11 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),
                          "avg_launch_us": step_s * 1e6 * (K if resident else 1), "us_per_step": step_s * 1e6,
                          "timing": "HIP events recorded by pf_run_device on the engine stream around its "
-                                   "filter kernels (pf_set_timing / pf_last_run_ms)",
+                                   "filter kernels (pf_set_timing / pf_last_run_ms)"
+                                   + ("; nx > 4: the step kernels' time from a second K-step window without "
+                                      "the covariance (the data's continuation), the covariance kernels' time is "
+                                      "the difference" if split_cov else ""),
+                         "cov_us_per_step": None if cov_ms is None else cov_ms * 1e3 / K,
                          "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src,
                          "valu": pmc_valu(wl.name, kname, step_s * 1e6)},
             "cpu_baseline": cpu,

@@ -408,7 +408,9 @@ __global__ void __launch_bounds__(DBS) k_dyn_step(StepParams p) {
         NStream<Real> ns(p.seed, i, nx, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, p.pbase);
         dyn_add_lower<Real>(xo, W + i, S, nx, P + L.LJ, ldiag, ns);
       }
-      if (p.xr_out) {  // the post-resample rows, for the device loop's covariance (pf_cov.h)
+      if (p.anc_out) {  // the post-resample rows for the device loop's covariance (pf_cov.h): by index
+        p.anc_out[(int64_t)r * p.N + i] = a;
+      } else if (p.xr_out) {  // ... or (jittered) by value
         Real* xr = (Real*)p.xr_out + (int64_t)r * nx * S + i;
         for (int d = 0; d < nx; ++d) xr[d * S] = xo[d * S];
       }

@@ -227,8 +227,9 @@ struct pf_handle {
   bool last_resident = false;  // the last pf_run_device ran k_resident
   // device-loop covariance for nx > 4 (pf_cov.h): post-resample rows, block partials, sums,
   // per-replicate arrival counters, and the launch geometry
-  void* xr = nullptr;
-  double* cov_part = nullptr;
+  void* xr = nullptr;        // post-resample rows (with jitter) ...
+  int32_t* anc = nullptr;    // ... or the ancestors of the post-resample slots (without)
+  void* cov_part = nullptr;  // [tc][R][nblk][P] block partials (doubles)
   double* cov_tot = nullptr;
   int cov_tc = 0;       // ring slots (steps) of partials
   int64_t cov_s0 = 0;   // first step of the pending chunk
@@ -537,7 +538,7 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
 // 4 waves over ~2048 waves per launch (or one block per replicate and block pair for nx > 48).
 // ---------------------------------------------------------------------------
 pf_status ensure_cov(pf_handle* h) {
-  if (h->xr) return PF_OK;
+  if (h->xr || h->anc) return PF_OK;
   CovParams& c = h->covp;
   c.N = h->N;
   c.Npad = h->Npad;
@@ -545,8 +546,11 @@ pf_status ensure_cov(pf_handle* h) {
   c.nb = (h->nx + 15) / 16;
   c.npairs = c.nb * (c.nb + 1) / 2;
   c.P = c.npairs * 256 + c.nb * 16 + 1;
-  c.nblk = (int)((h->N + COV_BLK - 1) / COV_BLK);
-  HIPCHK(hipMalloc(&h->xr, (size_t)h->R * h->nx * h->Npad * h->esz));
+  c.cpb = cov_chunks_per_block(h->N, h->R);
+  if (const char* e = std::getenv("PF_COV_CPB")) c.cpb = std::max(1, std::min(COV_CPB_MAX, std::atoi(e)));  // experiments
+  c.nblk = (int)((h->N + (int64_t)COV_BLK * c.cpb - 1) / ((int64_t)COV_BLK * c.cpb));
+  if (h->regularize) HIPCHK(hipMalloc(&h->xr, (size_t)h->R * h->nx * h->Npad * h->esz));
+  else HIPCHK(hipMalloc((void**)&h->anc, (size_t)h->R * h->N * sizeof(int32_t)));
   const size_t slot = (size_t)h->R * c.nblk * c.P * sizeof(double);
   h->cov_tc = (int)std::max<size_t>(1, std::min<size_t>(32, ((size_t)256 << 20) / slot));  // <= 256 MiB of ring
   HIPCHK(hipMalloc((void**)&h->cov_part, (size_t)h->cov_tc * slot));
@@ -579,6 +583,7 @@ pf_status flush_cov(pf_handle* h, double* d_covs) {
   const CovParams& c = h->covp;
   CovFin f;
   f.part = h->cov_part;
+  f.part_f32 = 0;
   f.tot = h->cov_tot;
   f.cov = d_covs + h->cov_s0 * h->R * h->nx * h->nx;
   f.R = h->R;
@@ -588,7 +593,8 @@ pf_status flush_cov(pf_handle* h, double* d_covs) {
   f.nb = c.nb;
   f.npairs = c.npairs;
   const unsigned nr = (unsigned)(h->cov_pending * h->R);
-  hipLaunchKernelGGL(k_cov_fin_sum, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
+  if (f.part_f32) hipLaunchKernelGGL(k_cov_fin_sum<float>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
+  else hipLaunchKernelGGL(k_cov_fin_sum<double>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cov_fin_out, dim3((unsigned)((h->nx * h->nx + 255) / 256), nr), dim3(256), 0, h->stream, f);
   HIPCHK(hipGetLastError());
@@ -605,9 +611,10 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, co
   const int R = h->R;
   if (h->cov_pending == 0) h->cov_s0 = s;
   if (s != h->cov_s0 + h->cov_pending) return fail(PF_E_ARG, "device-loop covariance: steps out of order");
-  c.part = h->cov_part + (size_t)h->cov_pending * R * c.nblk * c.P;
+  c.part = (double*)h->cov_part + (size_t)h->cov_pending * R * c.nblk * c.P;
   c.xs = xs;
   c.xr = h->xr;
+  c.anc = h->anc;
   c.lw = lw;
   c.flag = d_flags + s * R;
   c.lse = d_lse + s * R;
@@ -1072,7 +1079,7 @@ void pf_destroy(pf_handle* h) {
   for (double* q : h->lcum)
     if (q) (void)hipFree(q);
   for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
-                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->cov_part, (void*)h->cov_tot})
+                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->anc, (void*)h->cov_part, (void*)h->cov_tot})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1291,7 +1298,8 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     pf_status st = ensure_cov(h);
     if (st) return st;
     h->cov_pending = 0;
-    p.xr_out = h->xr;
+    p.xr_out = h->xr;  // one of the two: rows with jitter, ancestors without
+    p.anc_out = h->anc;
   }
   p.o_neff = d_neff;
   p.o_lse = d_lse;

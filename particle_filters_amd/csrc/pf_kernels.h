@@ -407,6 +407,9 @@ struct StepParams {
   // device-loop covariance for nx > 4 (pf_cov.h): a gathering launch also writes its post-resample
   // (post-jitter) rows here, [R][NX][Npad]; null: not wanted
   void* xr_out;
+  // ... or, without jitter (the post-resample row of slot i IS predicted row anc[i]), only the
+  // ancestor index of every slot, [R][N] (4 bytes instead of 4 nx per slot); null: not wanted
+  int32_t* anc_out;
 };
 
 struct Head {

@@ -592,7 +592,9 @@ k_step_grp(StepParams p) {
       aux0 += 1.0;
 #pragma unroll
       for (int j = 0; j < PER; ++j) auxj[j] += (double)x[j];
-      if (p.xr_out) {  // the post-resample rows, for the device loop's covariance (pf_cov.h)
+      if (p.anc_out) {  // the post-resample rows for the device loop's covariance (pf_cov.h): by index
+        if (q == 0) p.anc_out[(int64_t)r * p.N + i] = a;
+      } else if (p.xr_out) {  // ... or (jittered) by value
         Real* xr = (Real*)p.xr_out + (int64_t)r * NX * p.Npad;
 #pragma unroll
         for (int j = 0; j < PER; ++j) xr[(int64_t)(q * PER + j) * p.Npad + i] = x[j];
