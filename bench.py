@@ -420,7 +420,11 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
             "host_tracker_variant": {"ms_per_step": t_host_total * 1e3 / K, "tracker_ms_per_step": t_tr * 1e3 / K,
                                      "note": "EKF stepped on the host in NumPy, covariances uploaded, same device loop"},
             "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS,
+                         "traffic": pmc_traffic("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
+                                                "k_flow_wave" if per_particle else "k_ledh_fused")[0],
+                         "traffic_unit": "HBM bytes per filter step of the kernel (rocprofv3 FETCH_SIZE x2 + "
+                                         "WRITE_SIZE, profiles/pmc_traffic_<workload>.json)",
                          "kernel": ("whole LEDH job: k_ekf_seq + " + ("per step k_flow_wave (per-particle flow)"
                                                                       if per_particle else
                                                                       "k_setup/k_compose + per step k_ledh_fused"))
@@ -795,7 +799,8 @@ def main():
     ktmpl = wl.kernel_tmpl.split(",", 1)[1]
     if dyn:
         ktmpl = ",".join(ktmpl.split(",")[-2:])  # k_dyn_step<Real, TK, OK>
-    traffic, traffic_src = pmc_traffic(wl.name, kname)
+    pkey = wl.name + ("_fp64" if args.precision == "fp64" else "")  # profiles/pmc_*_<pkey>.json
+    traffic, traffic_src = pmc_traffic(pkey, kname)
     G, tile, lds = pf.geometry()
     workload_desc, data_desc = wl.describe(world)
     real = "float" if args.precision == "fp32" else "double"
@@ -897,7 +902,7 @@ def main():
                                       "the difference" if split_cov else ""),
                          "cov_us_per_step": None if cov_ms is None else cov_ms * 1e3 / K,
                          "traffic_unit": "HBM bytes per filter step", "traffic_source": traffic_src,
-                         "valu": pmc_valu(wl.name, kname, step_s * 1e6)},
+                         "valu": pmc_valu(pkey, kname, step_s * 1e6)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -288,6 +288,11 @@ struct pf_ledh_handle {
   int fused_nbk = 0, fused_ppb = 0;
   unsigned long long fphase = 0;
   unsigned long long *fwords = nullptr, *fpart = nullptr, *fcpart = nullptr;
+  int32_t* fanc = nullptr;  // [N] ancestors of the slots between fused steps
+  // run_impl's device buffers (tracker covariances, observations, outputs, flow tables), one
+  // allocation kept across runs: a run allocates only when it needs more than the last one
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
   unsigned int* ferr = nullptr;
   double *table = nullptr, *d_lams = nullptr, *diagS = nullptr, *out = nullptr, *unif = nullptr, *Lc = nullptr;
   // replayed draws for the next run (pf_ledh_set_run_replay): noise [T][N][nx], U [T]
@@ -544,6 +549,7 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
       h->fused_ppb = (int)ppb;
       if (hipMalloc((void**)&h->fwords, FMAX * 8) != hipSuccess || hipMalloc((void**)&h->fpart, 4 * FMAX * 8) != hipSuccess ||
           hipMalloc((void**)&h->fcpart, (size_t)FMAX * ops->fused_E * 8) != hipSuccess ||
+          hipMalloc((void**)&h->fanc, (size_t)h->N * sizeof(int32_t)) != hipSuccess ||
           hipMalloc((void**)&h->ferr, 8) != hipSuccess)
         return bail("fused step buffers");
       (void)hipMemset(h->fwords, 0, FMAX * 8);
@@ -583,7 +589,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
                     h->xbar, h->rp_noise, h->rp_unif})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)h->fwords, (void*)h->fpart, (void*)h->fcpart, (void*)h->ferr})
+  for (void* p : {(void*)h->fwords, (void*)h->fpart, (void*)h->fcpart, (void*)h->fanc, (void*)h->ferr, (void*)h->arena})
     if (p) (void)hipFree(p);
   if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->side) (void)hipStreamDestroy(h->side);
@@ -794,23 +800,35 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
   double* dE = nullptr;  // EKF inputs / outputs: x0 | P0 | Qt | Rt | x_final | P_final
   double* dX = nullptr;  // EDH: past means [T][nx]
   int32_t* df = nullptr;
-  auto cleanup = [&]() {
-    for (double* p : {dP, dZ, dU, dm, dc, de, dTab, dE, dX})
-      if (p) (void)hipFree(p);
-    if (df) (void)hipFree(df);
-  };
+  auto cleanup = [&]() {};  // the buffers live in the handle's arena
   const size_t ne = 2 * (size_t)nx + 3 * (size_t)nx * nx + (size_t)nz * nz;
-  bool ok = hipMalloc((void**)&dP, (size_t)T * nx * nx * 8) == hipSuccess &&
-            hipMalloc((void**)&dZ, (size_t)T * nz * 8) == hipSuccess &&
-            (!U || hipMalloc((void**)&dU, (size_t)T * nx * 8) == hipSuccess) &&
-            hipMalloc((void**)&dm, (size_t)T * nx * 8) == hipSuccess &&
-            hipMalloc((void**)&dc, (size_t)T * nx * nx * 8) == hipSuccess &&
-            hipMalloc((void**)&de, (size_t)T * 8) == hipSuccess && hipMalloc((void**)&df, (size_t)T * 4) == hipSuccess &&
-            (!ekf || hipMalloc((void**)&dE, ne * 8) == hipSuccess) &&
-            (!edh || hipMalloc((void**)&dX, (size_t)T * nx * 8) == hipSuccess);
-  if (!ok) {
-    cleanup();
-    return lfail(PF_E_HIP, "hipMalloc of run buffers failed");
+  const size_t tsz = TLayHost(nx, nz, h->L);
+  const bool tabled = h->shared || edh;
+  {
+    struct Piece { void** p; size_t b; };
+    const Piece pieces[] = {{(void**)&dP, (size_t)T * nx * nx * 8}, {(void**)&dZ, (size_t)T * nz * 8},
+                            {(void**)&dU, U ? (size_t)T * nx * 8 : 0}, {(void**)&dm, (size_t)T * nx * 8},
+                            {(void**)&dc, (size_t)T * nx * nx * 8}, {(void**)&de, (size_t)T * 8},
+                            {(void**)&df, (size_t)T * 4}, {(void**)&dE, ekf ? ne * 8 : 0},
+                            {(void**)&dX, edh ? (size_t)T * nx * 8 : 0}, {(void**)&dTab, tabled ? (size_t)T * tsz * 8 : 0}};
+    size_t need = 0;
+    for (const Piece& q : pieces) need += (q.b + 255) / 256 * 256;
+    if (need > h->arena_bytes) {
+      if (h->arena) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipStreamSynchronize(h->side);
+        (void)hipFree(h->arena);
+        h->arena = nullptr;
+        h->arena_bytes = 0;
+      }
+      if (hipMalloc((void**)&h->arena, need) != hipSuccess) return lfail(PF_E_HIP, "hipMalloc of run buffers failed");
+      h->arena_bytes = need;
+    }
+    size_t off = 0;
+    for (const Piece& q : pieces) {
+      *q.p = q.b ? (void*)(h->arena + off) : nullptr;
+      off += (q.b + 255) / 256 * 256;
+    }
   }
   pf_status st = PF_OK;
   do {
@@ -822,12 +840,6 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       break;
     }
     double *ex0 = dE, *eP0 = dE + nx, *eQ = eP0 + nx * nx, *eR = eQ + nx * nx, *exf = eR + nz * nz, *ePf = exf + nx;
-    const size_t tsz = TLayHost(nx, nz, h->L);
-    const bool tabled = h->shared || edh;
-    if (tabled && hipMalloc((void**)&dTab, (size_t)T * tsz * 8) != hipSuccess) {
-      st = lfail(PF_E_HIP, "hipMalloc of the run's flow tables failed");
-      break;
-    }
     // flow tables of steps [c0, c0 + n) (they depend on (P_k, z_k) only, not on the particles)
     auto tables = [&](int64_t c0, int64_t n, hipStream_t s) -> bool {
       if (!tabled) return true;
@@ -844,9 +856,12 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       }
       return h->ops->setup(fp, dTab + c0 * tsz, h->L, (int)n, s) == hipSuccess;
     };
-    // Device tracker: the EKF and the tables run on the side stream CH steps at a time, ahead of the
-    // particle loop, which waits for each chunk's event (the tracker never needs the particles).
+    // Device tracker: the EKF and the tables run on the side stream in chunks of steps, ahead of the
+    // particle loop, which waits for each chunk's event (the tracker never needs the particles).  The
+    // chunks grow 2, 4, 8, 16, 16, ...: the loop starts after two EKF steps, not sixteen.
     const int64_t CH = 16;
+    std::vector<int64_t> cbeg;  // first step of each chunk
+    for (int64_t c0 = 0, n = 2; c0 < T; c0 += n, n = std::min(CH, 2 * n)) cbeg.push_back(c0);
     std::vector<hipEvent_t> evs;
     if (ekf) {
       if (hipMemcpyAsync(ex0, ekf->x0, nx * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
@@ -865,8 +880,8 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         break;
       }
       evs.push_back(up);
-      for (int64_t c0 = 0; c0 < T && st == PF_OK; c0 += CH) {
-        const int64_t n = std::min(CH, T - c0);
+      for (size_t k = 0; k < cbeg.size() && st == PF_OK; ++k) {
+        const int64_t c0 = cbeg[k], n = (k + 1 < cbeg.size() ? cbeg[k + 1] : T) - c0;
         hipEvent_t ev;
         if (h->ops->ekf(h->Pm, exf, ePf, eQ, eR, dZ + c0 * nz, n, dP + c0 * nx * nx, exf, ePf,
                         edh ? dX + c0 * nx : nullptr, h->side) != hipSuccess ||
@@ -885,50 +900,91 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     const bool fused_run = h->fused_nbk > 0 && dTab;
     std::optional<GridOrderScope> order;  // no overlap with another handle's grid
     if (fused_run) order.emplace(h->device, h->stream);
+    // fused path: launch t also reduces step t - 1's moments (its P5), whose mean is step t's
+    // shift; a P5-only launch ends the run.  cur: step t-1's shift buffer, oth: its mean's
+    double* cur = h->mean_prev;
+    double* oth = h->mean;
+    // and the state between its steps is (the last step's flow rows, ancestors): xa holds the rows
+    // the next step starts from, xb takes its flow rows
+    double* xa = h->x;
+    double* xb = h->x_alt;
+    auto fused_common = [&](FusedParams& fp) {
+      fp.stat = h->stat;
+      fp.words = h->fwords;
+      fp.part = h->fpart;
+      fp.cpart = h->fcpart;
+      fp.err = h->ferr;
+      fp.phase0 = h->fphase;
+      h->fphase += 4;
+      fp.ratio = h->ratio;
+      fp.nbk = h->fused_nbk;
+      fp.ppb = h->fused_ppb;
+    };
+    size_t next_chunk = 0;
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
-      if (ekf && t % CH == 0 && hipStreamWaitEvent(h->stream, evs[1 + t / CH], 0) != hipSuccess) {
+      if (ekf && next_chunk < cbeg.size() && t == cbeg[next_chunk] &&
+          hipStreamWaitEvent(h->stream, evs[1 + next_chunk++], 0) != hipSuccess) {
         st = lfail(PF_E_HIP, "run: stream wait failed");
         break;
       }
-      if (h->fused_nbk > 0 && dTab) {  // the whole step in one launch (pf_ledh_fused.h)
-        FusedParams fp;
+      if (fused_run) {  // the whole step in one launch (pf_ledh_fused.h)
+        FusedParams fp{};
         fp.f = flow_params(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise,
                            replay ? h->rp_noise + t * h->N * nx : nullptr, nullptr);
         fp.f.table = dTab + t * tsz;
+        fp.f.x_in = xa;
+        fp.f.x_out = xb;
+        fp.anc_in = t > 0 ? h->fanc : nullptr;
+        fp.anc_out = h->fanc;
         fp.rp_unif = replay ? h->rp_unif + t : nullptr;
         fp.f.epoch = ++h->epoch;
         fp.ep_res = ++h->epoch;
-        fp.x_res = h->x;
         fp.w_out = h->w_alt;
-        fp.shift = h->mean_prev;
-        fp.mean = h->mean;
-        fp.o_mean = dm + t * nx;
-        fp.o_cov = dc + t * nx * nx;
+        fp.step = 1;
+        fp.p5 = t > 0;
+        if (t > 0) {
+          fp.shift5 = cur;
+          fp.mean5 = oth;
+          fp.o_mean5 = dm + (t - 1) * nx;
+          fp.o_cov5 = dc + (t - 1) * nx * nx;
+          std::swap(cur, oth);
+        }
+        fp.shift = cur;
         fp.o_ess = de + t;
         fp.o_flag = df + t;
-        fp.stat = h->stat;
-        fp.cdf = h->cdf;
-        fp.words = h->fwords;
-        fp.part = h->fpart;
-        fp.cpart = h->fcpart;
-        fp.err = h->ferr;
-        fp.phase0 = h->fphase;
-        h->fphase += 4;
-        fp.ratio = h->ratio;
-        fp.nbk = h->fused_nbk;
-        fp.ppb = h->fused_ppb;
+        fused_common(fp);
         if (h->ops->fused(fp, h->stream) != hipSuccess) {
           st = lfail(PF_E_HIP, "run: fused step launch failed");
           break;
         }
         std::swap(h->w, h->w_alt);
-        std::swap(h->mean, h->mean_prev);
+        std::swap(xa, xb);
         continue;
       }
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise,
                         replay ? h->rp_noise + t * h->N * nx : nullptr, nullptr, de + t, df + t,
                         dTab ? dTab + t * tsz : nullptr);
       if (st == PF_OK) st = enqueue_finish(h, replay ? h->rp_unif + t : nullptr, dm + t * nx, dc + t * nx * nx);
+    }
+    if (fused_run && st == PF_OK) {  // the last step's outputs and the materialised state
+      FusedParams fp{};
+      fp.f.N = h->N;
+      fp.f.Npad = h->Npad;
+      fp.f.x_in = xa;
+      fp.anc_in = h->fanc;
+      fp.x_res = xb;
+      h->x = xb;
+      h->x_alt = xa;
+      fp.step = 0;
+      fp.p5 = 1;
+      fp.shift5 = cur;
+      fp.mean5 = oth;
+      fp.o_mean5 = dm + (T - 1) * nx;
+      fp.o_cov5 = dc + (T - 1) * nx * nx;
+      fused_common(fp);
+      if (h->ops->fused(fp, h->stream) != hipSuccess) st = lfail(PF_E_HIP, "run: fused tail launch failed");
+      h->mean_prev = oth;  // the latest mean: the next moments' shift
+      h->mean = cur;
     }
     if (order) order->end();
     if (ekf) (void)hipStreamSynchronize(h->side);

@@ -1,72 +1,70 @@
-// One LEDH / EDH step of the shared-Jacobian (linear h) path in ONE launch: the affine flow,
-// the weights (ledh.py:186-195 / edh.py:287-297), ESS and decision (ledh.py:39-41, 201-203),
-// systematic resampling (ledh.py:25-37, 204-206) and the posterior moments (ledh.py:209,
-// 217-224) — the work of k_flow_affine, k_weights_small, k_gather, k_mom_part and k_mom_final,
+// One LEDH / EDH step of the shared-Jacobian (linear h) path in ONE launch with ONE grid barrier:
+// the affine flow, the weights (ledh.py:186-195 / edh.py:287-297), ESS and decision (ledh.py:39-41,
+// 201-203), systematic resampling (ledh.py:25-37, 204-206) and the posterior moments (ledh.py:209,
+// 217-224) - the work of k_flow_affine, k_weights_small, k_gather, k_mom_part and k_mom_final,
 // whose floors (10-17 us each on 1e4 particles, fewer waves than SIMDs) dominated config 5.
 //
-// NBK co-resident workgroups (<= one per CU), each owning PPB consecutive particles (and the
-// same PPB destination slots), meet at grid barriers (per-workgroup phase words; data handed
-// between workgroups goes through write-through stores / loads, as in k_resident):
-//   P1  flow of its particles -> x_out (SoA, write-through), log weights in LDS; max     | B1
-//   P2  global max M; e = exp(l - M); workgroup sum e, sum e^2, inclusive scan in LDS   | B2
-//   P3  S = sum e, ESS = S^2 / sum e^2, decision; on a resample its slice of the global
-//       CDF c_j = (offset + scan_j) / S (c = 1 for the last particle, the reference's
-//       clamp) and its last value are published                                       | B3
-//   P4  its slots: ancestors by a two-level search (source workgroup over the published
-//       last values, then inside the source slice staged in LDS) = searchsorted(cdf,
-//       (U + i)/N, 'right'); rows copied into x_res (or copied through with w = e/S), and
-//       the one-pass shifted moment partials of the rows (4x4 register blocks)          | B4
-//   P5  the NOUT = NX + NX(NX+1)/2 output entries, 16 per round, over the NBK partials;
-//       workgroup 0 also writes ESS / decision.
-// The new state always lands in x_res (the previous state's buffer, dead after P1) and w_out.
+// NBK co-resident workgroups (<= one per CU), each owning PPB consecutive particles (slots):
+//   P5' the PREVIOUS step's output entries (NX + NX(NX+1)/2) over the NBK moment partials it left,
+//       spread over every workgroup; its mean is this step's moment shift (written through, read
+//       after B1).  Its loads are issued together with the parameter block's LDS staging loads.
+//   P1  flow of its slots.  The state enters as (rows, ancestors): slot i starts from row anc[i]
+//       of the previous step's flow output - the previous resample is applied by this gather, no
+//       separate copy.  Flow rows -> x_out (write-through; the first FCH also stay in LDS), log
+//       weights in LDS; the workgroup max
+//   P2  e = exp(l - m) relative to the WORKGROUP max, sum e, sum e^2 and the inclusive scan in LDS;
+//       published: (m, sum e, sum e^2, last scan value)                                   | B1
+//   P3  every workgroup combines the NBK partials in one fixed order: normaliser S, ESS,
+//       decision, the exclusive prefix O_k of the scaled workgroup sums and every workgroup's
+//       scale, hence its own CDF slice c_j = (O_b + f_b scan_j) / S (c = 1 for the last particle,
+//       the reference's clamp) and its predecessor's last value.  Resampling is SOURCE-driven:
+//       particle j is the ancestor of the slots {i : max(last_{b-1}, c_{j-1}) <= (U + i)/N < c_j}
+//       (the last particle of the last workgroup also takes positions past the end, as the
+//       destination search's clamp did) - exactly the ancestors of the two-level
+//       searchsorted(cdf, (U+i)/N, 'right') over the slices; the workgroup counts them (positions
+//       below a CDF value, with the reference's comparison where it is close) and writes its index
+//       into those slots of anc_out (4 bytes a slot: the imbalance of a degenerate resample is
+//       cheap).  No resample: identity ancestors, w = e / S.
+//   P4  moment partials of the reported set from the workgroup's OWN rows: weights n_j / N (n_j
+//       = offspring count) after a resample - the sums over the post-resample slots - or e_j / S;
+//       one-pass, shifted by the previous mean, 4x4 register blocks; left for the next launch.
+// A run ends with a tail launch (step = 0): the last P5' and the materialised state
+// x_res[i] = rows[anc[i]].
 #pragma once
 #include "pf_ledh_kernels.h"
 
 namespace pf {
 namespace ledh {
 
-// workgroup: 64 particles per flow round at GL lanes each (512 lanes for L96's 8-lane groups)
+// workgroup: FCH = 64 particles per flow round at GL lanes each (512 lanes for 8-lane groups)
 template <int NX>
 struct FusedBlk {
   static constexpr int FB = Grp<NX>::GL >= 8 ? 512 : 256;
+  static constexpr int FCH = FB / Grp<NX>::GL;
 };
 constexpr int FMAX = 256;                      // max workgroups (one per CU, co-resident)
 constexpr int FPPB = 256;                      // max particles per workgroup (N <= FMAX * FPPB)
-constexpr int FMC = 64;                        // particles per moment chunk (staged in LDS)
 constexpr unsigned FSPIN = 1u << 24;           // barrier spin limit (then the launch fails)
-constexpr int FNST = 4;                        // source CDF slices staged in LDS per moment chunk
-#ifndef PF_LEDH_LDS
-#define PF_LEDH_LDS 1                          // parameters and composed flow staged in LDS (P1)
-#endif
-
-// diagnostic phase stamps (PF_STAMPS builds only): s_memrealtime (100 MHz) per workgroup
-#ifdef PF_STAMPS
-constexpr int FST = 12;
-__device__ unsigned long long g_ledh_stamps[FMAX * FST];
-#define LF_STAMP(k)                                                                          \
-  do {                                                                                       \
-    if (threadIdx.x == 0) g_ledh_stamps[blockIdx.x * FST + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define LF_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
 
 struct FusedParams {
-  FlowParams f;                  // x_in (previous state), x_out (flow scratch), w_in, table, ...
-  double* x_res;                 // [NX][Npad] the new state (== f.x_in)
+  FlowParams f;                  // x_in: the rows slots start from (previous flow output, or the state),
+                                 // x_out: this step's flow rows, w_in, table, ...
+  const int32_t* anc_in;         // [N] slot i starts from row anc_in[i] of f.x_in; null: row i
+  int32_t* anc_out;              // [N] this step's ancestors (identity without a resample)
+  double* x_res;                 // tail launch: [NX][Npad] the materialised state rows[anc[i]]
   double* w_out;                 // [N] the new weights
-  const double* shift;           // [NX] previous posterior mean (moment shift)
-  double* mean;                  // [NX] new posterior mean (next shift)
-  double* o_mean;                // [NX] or null
-  double* o_cov;                 // [NX][NX] or null
-  double* o_ess;                 // or null
+  const double* shift;           // [NX] this step's moment shift: the previous posterior mean (== mean5 when p5)
+  int step;                      // 1: run a filter step; 0: a run's tail (P5' and the materialised state)
+  int p5;                        // 1: reduce the previous step's moment partials (cpart) first
+  const double* shift5;          // [NX] the previous step's shift
+  double* mean5;                 // [NX] the previous step's posterior mean (write-through: read after B1)
+  double* o_mean5;               // [NX] or null: the previous step's outputs
+  double* o_cov5;                // [NX][NX] or null
+  double* o_ess;                 // or null: this step's
   int32_t* o_flag;               // or null
   double* stat;                  // [4] ess, flag, sw
-  double* cdf;                   // [N] the global CDF (resample steps)
   unsigned long long* words;     // [NBK] barrier phase words (monotonic across launches)
-  unsigned long long* part;      // [4][FMAX] workgroup max / sum e / sum e^2 / last CDF value (bits)
+  unsigned long long* part;      // [4][FMAX] workgroup max / sum e / sum e^2 / last scan value (bits)
   unsigned long long* cpart;     // [NBK][E] moment partials (double bits)
   unsigned int* err;             // barrier timeout flag
   unsigned long long phase0;     // phase word base of this launch
@@ -107,60 +105,217 @@ __device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long lo
   }
 }
 
+// #{ i in [0, N) : (U + i) / N < x } with the destination search's comparison (pos = (U + i) / N
+// in fp64; x = -inf / +inf give 0 / N).  Exactly, (U + i) / N < x <=> i < y = x N - U; the fp64
+// division can only disagree when y is within ~1e-11 of an integer, so only there are the
+// candidate positions evaluated the reference's way.
+__device__ __noinline__ int64_t fcount_exact(double x, double U, int64_t N, int64_t c) {
+  const double Nd = (double)N;
+  while (c > 0 && (U + (double)(c - 1)) / Nd >= x) --c;
+  while (c < N && (U + (double)c) / Nd < x) ++c;
+  return c;
+}
+__device__ __forceinline__ int64_t fcount_below(double x, double U, int64_t N) {
+  if (!(x > -INFINITY)) return 0;
+  if (x == INFINITY) return N;
+  const double y = fma(x, (double)N, -U);
+  const double fl = floor(y), d = y - fl;
+  const int64_t c = min(max((int64_t)fl + 1, (int64_t)0), N);
+  if (d > 1e-7 && d < 1.0 - 1e-7) return c;
+  return fcount_exact(x, U, N, c);
+}
+
+// P5': the NOUT = NX + NX(NX+1)/2 output entries of the previous step over the NBK partials it left
+// (ledh.py:209, 217-224).  Entry q is reduced by a group of LPE lanes (64, or 32 / 16 so that every
+// entry gets a group in one round), lane l summing partials l, l + LPE, ... (loaded in one batch:
+// p5_load issues them, p5_finish consumes them, so their latency can overlap other loads), then a
+// fixed xor tree: the same order in every run.  The partials were written by the previous launch
+// (visible after the kernel boundary): plain loads.
+constexpr int P5K = 8;  // partials per lane in one batch
+template <int NX, int FB>
+struct P5 {
+  static constexpr int NOUT = NX + Mom<NX>::NP;
+  int lpe, groups, gl, qo, d, e, src[4];
+  bool live;
+  __device__ P5(const FusedParams& p, int round) {
+    const int t = threadIdx.x;
+    lpe = (p.nbk * (FB / 64) >= NOUT) ? 64 : (p.nbk * (FB / 32) >= NOUT ? 32 : 16);
+    groups = FB / lpe;
+    gl = t % lpe;
+    qo = (blockIdx.x + round * p.nbk) * groups + t / lpe;
+    live = qo < NOUT;
+    d = 0;
+    e = 0;
+    if (live && qo >= NX) pair_of(qo - NX, NX, &d, &e);
+    src[0] = 0;
+    src[1] = 1 + (qo < NX ? qo : d);
+    src[2] = 1 + e;
+    src[3] = qo >= NX ? 1 + NX + (qo - NX) : 0;
+  }
+  static __device__ int rounds(const FusedParams& p) {
+    const int lpe = (p.nbk * (FB / 64) >= NOUT) ? 64 : (p.nbk * (FB / 32) >= NOUT ? 32 : 16);
+    const int per = p.nbk * (FB / lpe);
+    return (NOUT + per - 1) / per;
+  }
+  __device__ void load(const FusedParams& p, int k0, double (&v)[P5K][4]) const {
+    const double* cp5 = (const double*)p.cpart;
+#pragma unroll
+    for (int r = 0; r < P5K; ++r) {
+      const int k = k0 + gl + r * lpe;
+      const bool ok = live && k < p.nbk;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) v[r][f] = ok ? cp5[(int64_t)k * Mom<NX>::E + src[f]] : 0.0;
+    }
+  }
+  __device__ void finish(const FusedParams& p, double (&v)[P5K][4]) const {
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0;; k0 += P5K * lpe) {
+#pragma unroll
+      for (int r = 0; r < P5K; ++r)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) tot[f] += v[r][f];
+      if (k0 + P5K * lpe >= p.nbk) break;
+      load(p, k0 + P5K * lpe, v);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      for (int o = 1; o < lpe; o <<= 1) tot[f] += __shfl_xor(tot[f], o);
+    if (live && gl == 0) {
+      const double sw = tot[0];
+      if (qo < NX) {
+        const double mv = p.shift5[qo] + tot[1] / sw;
+        f_std(p.mean5 + qo, mv);
+        if (p.o_mean5) p.o_mean5[qo] = mv;
+      } else {
+        const double c = tot[3] / sw - (tot[1] / sw) * (tot[2] / sw);
+        if (p.o_cov5) {
+          p.o_cov5[d * NX + e] = c;
+          p.o_cov5[e * NX + d] = c;
+        }
+      }
+    }
+  }
+};
+
 template <int NX, int NZ, int TK>
 __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) {
   constexpr int FB = FusedBlk<NX>::FB;
+  constexpr int FCH = FusedBlk<NX>::FCH;  // particles per flow round = rows per moment chunk
   using MM = Mom<NX>;
   using MB = MomBlk<NX>;
-  constexpr int GL = Grp<NX>::GL;
-  constexpr int FCH = FB / GL;  // particles per flow round
+  using L = Lay<NX, NZ>;
+  using TL = TLay<NX, NZ>;
+  constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  constexpr int XW = MB::XW;
+  static_assert(MB::NPAIR * MB::SL <= FB, "block pairs x slices fit the workgroup");
   __shared__ double lws[FPPB];   // log weights, then e, of this workgroup's particles
   __shared__ double scan[FPPB];  // inclusive scan of e
   __shared__ double red[64];
-  __shared__ double boff[FMAX + 1];
-  __shared__ double xs[FMC * MB::XW];
-  __shared__ double ws[FMC];
+  __shared__ double boff[FMAX + 1];   // exclusive prefix of the scaled workgroup sums (+ total)
+  __shared__ double xs[FCH * XW];     // raw rows of a chunk (the first flow round's stay from P1)
+  __shared__ double ws[FCH];
+  __shared__ int64_t shi[FPPB];       // resample: end of each particle's slot range
   __shared__ double mred[MB::SL][MB::NPAIR][16];
+  __shared__ double pms[L::SIZE];     // the parameter block (the parts the flow reads)
+  __shared__ double afs[TL::AFF_SIZE];  // the composed flow
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t N = p.f.N, Npad = p.f.Npad;
   const int64_t i0 = (int64_t)b * p.ppb;
   const int n = (int)max((int64_t)0, min((int64_t)p.ppb, N - i0));  // this workgroup's particles
+  // the first flow round's slot, source row and weight: loaded first, their latency under the staging
+  const int slot1 = t / GL;
+  const int64_t i1 = slot1 < n ? i0 + slot1 : i0;
+  const int64_t src1 = (p.step && p.anc_in) ? (int64_t)p.anc_in[i1] : i1;
+  const double w1 = p.step ? p.f.w_in[i1] : 0.0;
+  double x1[PER];  // and its row's components of this lane
+#pragma unroll
+  for (int jj = 0; jj < PER; ++jj) {
+    const int a = (t % GL) * PER + jj;
+    x1[jj] = (p.step && a < NX) ? p.f.x_in[(int64_t)a * Npad + src1] : 0.0;
+  }
+  double v5[P5K][4];
+  const P5<NX, FB> p5_0(p, 0);
+  if (p.p5) p5_0.load(p, 0, v5);  // issued first: its latency overlaps the staging loads below
+  if (!p.step) {  // a run's tail: the last step's outputs and the materialised state rows[anc[i]]
+    if (p.p5) {
+      p5_0.finish(p, v5);
+      for (int r = 1; r < P5<NX, FB>::rounds(p); ++r) {
+        const P5<NX, FB> q5(p, r);
+        q5.load(p, 0, v5);
+        q5.finish(p, v5);
+      }
+    }
+    if (p.anc_in)
+      for (int e = t; e < n * NX; e += FB) {
+        const int j = e % n, d = e / n;
+        p.x_res[(int64_t)d * Npad + i0 + j] = p.f.x_in[(int64_t)d * Npad + p.anc_in[i0 + j]];
+      }
+    return;
+  }
   const unsigned long long ph = p.phase0;
   LF_STAMP(0);
 
-  // ---- P1: flow --------------------------------------------------------------------
-  // The parameter block and the composed flow are read by every lane group many times over
-  // (H, D, QL, ... at lane-dependent offsets): staged once per workgroup in LDS, so the
-  // per-particle chain waits on LDS instead of L2 round trips at one wave per SIMD.
-#if PF_LEDH_LDS
-  using L = Lay<NX, NZ>;
-  using TL = TLay<NX, NZ>;
-  __shared__ double pms[L::SIZE];
-  __shared__ double afs[TL::AFF_SIZE];
+  // ---- staging: the parameter block and the composed flow are read by every lane group many times
+  // over (H, D, QL, ... at lane-dependent offsets): copied once per workgroup into LDS, so the
+  // per-particle chain waits on LDS instead of L2 round trips at one wave per SIMD.  Only the parts
+  // the flow reads (the diagonals of chol(Q) and Q^{-1} when Q is diagonal), in batches of loads.
   {
     const bool qd = p.f.q_diag != 0;
-    auto need = [&](int k) {
-      if (k < L::EX) return TK != PF_TRANS_L96;             // A (linear g)
-      if (k < L::AC) return true;                           // F, dt, H, c
-      if (k < L::LQ) return false;                          // acoustic geometry (not a linear h)
-      if (k < L::R) {                                       // chol(Q), Q^{-1}: the diagonal when diagonal
-        const int e = (k - L::LQ) % (NX * NX);
-        return !qd || (e / NX == e % NX);
-      }
-      return k >= L::RI;                                    // R^{-1}
-    };
-    for (int k = t; k < L::SIZE; k += FB)
-      if (need(k)) pms[k] = p.f.Pm[k];
+    constexpr int nA = TK != PF_TRANS_L96 ? NX * NX : 0;
+    constexpr int n0 = L::AC - L::EX;  // F, dt, H, c
+    const int nq = qd ? NX : NX * NX;  // per chol(Q) and Q^{-1}
+    constexpr int nR = NZ * NZ;        // R^{-1}
+    const int tot = nA + n0 + 2 * nq + nR + TL::AFF_SIZE;
     const double* __restrict__ afg = p.f.table + TL::aff(p.f.L);
-    for (int k = t; k < TL::AFF_SIZE; k += FB) afs[k] = afg[k];
-    __syncthreads();
+    auto src_of = [&](int f, bool& to_af) -> int {  // flat staging index -> source offset
+      to_af = false;
+      if (f < nA) return L::A + f;
+      f -= nA;
+      if (f < n0) return L::EX + f;
+      f -= n0;
+      if (f < 2 * nq) {
+        const int m = f / nq, r = f % nq;
+        return (m == 0 ? L::LQ : L::QI) + (qd ? r * NX + r : r);
+      }
+      f -= 2 * nq;
+      if (f < nR) return L::RI + f;
+      to_af = true;
+      return f - nR;
+    };
+    constexpr int SB = 8;
+    for (int f0 = 0; f0 < tot; f0 += SB * FB) {
+      double sv[SB];
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+        const int f = f0 + t + r * FB;
+        bool af = false;
+        const int k = f < tot ? src_of(f, af) : 0;
+        sv[r] = f < tot ? (af ? afg[k] : p.f.Pm[k]) : 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+        const int f = f0 + t + r * FB;
+        bool af = false;
+        const int k = f < tot ? src_of(f, af) : 0;
+        if (f < tot) {
+          if (af) afs[k] = sv[r];
+          else pms[k] = sv[r];
+        }
+      }
+    }
   }
-  const double* Pm_f = pms;
-  const double* af_f = afs;
-#else
-  const double* Pm_f = p.f.Pm;
-  const double* af_f = p.f.table + TLay<NX, NZ>::aff(p.f.L);
-#endif
+  if (p.p5) {  // the previous step's outputs and mean (= this step's shift)
+    p5_0.finish(p, v5);
+    for (int r = 1; r < P5<NX, FB>::rounds(p); ++r) {
+      const P5<NX, FB> q5(p, r);
+      q5.load(p, 0, v5);
+      q5.finish(p, v5);
+    }
+  }
+  __syncthreads();
+  LF_STAMP(1);
+
+  // ---- P1: flow --------------------------------------------------------------------
   double m = -INFINITY;
   {
     const int q = t % GL, slot = t / GL, base = lane - q;
@@ -168,9 +323,32 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       const int j = c0 + slot;
       const bool live = j < n;
       // whole lane groups stay together; dead groups run particle i0 (results discarded)
-      const double l = flow_affine_particle<NX, NZ, TK, true>(p.f, Pm_f, af_f, live ? i0 + j : i0, q, base);
-      if (live && q == 0) lws[j] = l;
-      if (live) m = fmax(m, l);
+      const int64_t i = live ? i0 + j : i0;
+      // the previous step's resample: the slot starts from its ancestor's row
+      const int64_t src = c0 == 0 ? src1 : (p.anc_in ? (int64_t)p.anc_in[i] : i);
+      const double wi = c0 == 0 ? w1 : p.f.w_in[i];
+      double eta[PER];
+      const double l = flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, c0 == 0 ? x1 : nullptr);
+#ifdef PF_STAMPS
+      asm volatile("" ::"v"(l));
+      if (c0 == 0) LF_STAMP(11);
+#endif
+      if (live) {
+#pragma unroll
+        for (int jj = 0; jj < PER; ++jj) {
+          const int a = q * PER + jj;
+          if (a < NX) wt_store(p.f.x_out + (int64_t)a * Npad + i, eta[jj]);  // the next step's gather
+          if (c0 == 0 && a < XW) xs[j * XW + a] = a < NX ? eta[jj] : 0.0;
+        }
+        if (q == 0) lws[j] = l;
+        m = fmax(m, l);
+      }
+    }
+    if constexpr (GL * PER < XW) {  // pad columns past the lane groups' components
+      for (int e = t; e < FCH * (XW - GL * PER); e += FB) {
+        const int j = e / (XW - GL * PER), a = GL * PER + e % (XW - GL * PER);
+        xs[j * XW + a] = 0.0;
+      }
     }
   }
   m = block_reduce_max(m, red);
@@ -206,17 +384,19 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     f_st(p.part + 0 * FMAX + b, m);
     f_st(p.part + 1 * FMAX + b, S_b);
     f_st(p.part + 2 * FMAX + b, S2_b);
+    f_st(p.part + 3 * FMAX + b, scan[n - 1]);
   }
-  LF_STAMP(1);
-  if (!f_barrier(p, ph + 1)) return;
   LF_STAMP(2);
+  if (!f_barrier(p, ph + 1)) return;
+  LF_STAMP(3);
 
-  // ---- P3: global normaliser, ESS, decision; the CDF slice on a resample -----------------
-  double mk = -INFINITY, sk = 0.0, s2k = 0.0;
+  // ---- P3: global normaliser, ESS, decision; this slice of the CDF; the ancestors -----------
+  double mk = -INFINITY, sk = 0.0, s2k = 0.0, slk = 0.0;
   if (t < p.nbk) {
     mk = f_ld(p.part + 0 * FMAX + t);
     sk = f_ld(p.part + 1 * FMAX + t);
     s2k = f_ld(p.part + 2 * FMAX + t);
+    slk = f_ld(p.part + 3 * FMAX + t);
   }
   const double M = block_reduce_max(sk > 0.0 ? mk : -INFINITY, red);
   const double fk = (sk > 0.0) ? exp(mk - M) : 0.0;
@@ -228,43 +408,63 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     double off = 0.0;
     for (int k = 0; k < wv; ++k) off += red[k];
     if (t < p.nbk) boff[t] = off + inc - v;  // exclusive prefix of the scaled workgroup sums
-    if (t == b) red[8] = fk;  // this workgroup's scale e^(m_b - M)
     if (t == FB - 1) boff[FMAX] = off + inc;  // total
+    __syncthreads();
+    if (t == b) red[8] = fk;  // this workgroup's scale e^(m_b - M)
+    // the predecessor's last CDF value, as that workgroup evaluates its own slice
+    if (t + 1 == b) red[9] = (boff[t] + fk * slk) / boff[FMAX];
     __syncthreads();
   }
   const double S = boff[FMAX];
   const double fb = red[8];
+  const double lastprev = b > 0 ? red[9] : -INFINITY;
   const double E2 = block_reduce_sum(s2k * fk * fk, red);
   const double ess = 1.0 / (E2 / (S * S));
   const bool flag = (p.ratio > 0.0) && (ess < p.ratio * (double)N);
-  if (flag) {
-    const double Ob = boff[b];
-    for (int j = t; j < n; j += FB) wt_store(p.cdf + i0 + j, (i0 + j == N - 1) ? 1.0 : (Ob + fb * scan[j]) / S);
-    if (t == 0) f_st(p.part + 3 * FMAX + b, (b == p.nbk - 1) ? 1.0 : (Ob + fb * scan[n - 1]) / S);
-    LF_STAMP(5);
-    if (!f_barrier(p, ph + 3)) return;
-    LF_STAMP(6);
-    if (t < p.nbk) boff[t] = f_ld(p.part + 3 * FMAX + t);  // last CDF value of every workgroup
-    __syncthreads();
+  if (b == 0 && t == 0) {
+    p.stat[0] = ess;
+    p.stat[1] = flag ? 1.0 : 0.0;
+    p.stat[2] = S;
+    if (p.o_ess) *p.o_ess = ess;
+    if (p.o_flag) *p.o_flag = flag ? 1 : 0;
   }
-
-  // ---- P4: this workgroup's slots -> x_res, staged rows, moment partials ------------------
-  __shared__ double slice[FNST * FPPB];
-  __shared__ int anc[FMC];
-  __shared__ int krange[2];
-  // ledh.py:28: the step's U (Philox, as k_gather; or the replayed host draw)
-  const double U = flag ? (p.rp_unif ? *p.rp_unif : uniform53(p.f.seed, 0u, 0u, p.ep_res)) : 0.0;
   const double dN = (double)N;
-  // first workgroup whose last CDF value exceeds pos (the last one if none)
-  auto src_block = [&](double pos) {
-    int lo = 0, hi = p.nbk;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (pos < boff[mid]) hi = mid; else lo = mid + 1;
+  const double Ob = boff[b];
+  int64_t slo0 = 0;
+  if (flag) {
+    // ledh.py:28: the step's U (Philox, as k_gather; or the replayed host draw)
+    const double U = p.rp_unif ? *p.rp_unif : uniform53(p.f.seed, 0u, 0u, p.ep_res);
+    for (int j = t; j < n; j += FB) {
+      const double c = (i0 + j == N - 1) ? 1.0 : (Ob + fb * scan[j]) / S;
+      shi[j] = (b == p.nbk - 1 && j == n - 1) ? N : fcount_below(c, U, N);
     }
-    return lo < p.nbk ? lo : p.nbk - 1;
-  };
-  double a0acc = 0.0, a1acc = 0.0;
+    slo0 = fcount_below(lastprev, U, N);
+    __syncthreads();
+    // slots [slo0, shi[n-1]): slot s takes the first own particle j with s < shi[j] - a binary
+    // search for the thread's first slot, then a cursor (slots rise by FB per iteration: a
+    // degenerate resample, one particle over most slots, costs O(1) per slot)
+    const int64_t s_end = shi[n - 1];
+    int jc = 0;
+    if (slo0 + t < s_end) {
+      int hi = n - 1;
+      while (jc < hi) {
+        const int mid = (jc + hi) >> 1;
+        if (slo0 + t < shi[mid]) hi = mid; else jc = mid + 1;
+      }
+    }
+    for (int64_t s = slo0 + t; s < s_end; s += FB) {
+      while (shi[jc] <= s) ++jc;
+      p.anc_out[s] = (int32_t)(i0 + jc);
+    }
+  } else {
+    for (int j = t; j < n; j += FB) p.anc_out[i0 + j] = (int32_t)(i0 + j);
+  }
+  for (int j = t; j < n; j += FB) p.w_out[i0 + j] = flag ? 1.0 / dN : (fb * lws[j]) / S;
+  LF_STAMP(4);
+
+  // ---- P4: moment partials of the reported set from the own rows --------------------------
+  // after a resample particle j stands for its n_j slots (weight n_j / N): the same sums as over
+  // the post-resample slots; otherwise its normalised weight
   const int pair = t % MB::NPAIR, sl = t / MB::NPAIR;
   int bi = 0, bj = 0;
   {
@@ -272,109 +472,80 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
     bj = bi + rem;
   }
+  double shb_i[4], shb_j[4];  // the shift of this thread's two 4-blocks (written by P5' of other
+                              // workgroups this launch: write-through loads after B1)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    shb_i[k] = 4 * bi + k < NX ? f_ldd(p.shift + 4 * bi + k) : 0.0;
+    shb_j[k] = 4 * bj + k < NX ? f_ldd(p.shift + 4 * bj + k) : 0.0;
+  }
+  double a0acc = 0.0, a1[4] = {0.0, 0.0, 0.0, 0.0};  // W (pair 0), S1 of block bi (diagonal pairs)
+  const bool diagp = bi == bj;
   double acc[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = 0.0;
-  for (int c0 = 0; c0 < n; c0 += FMC) {
-    const int cn = min(FMC, n - c0);
-    if (flag) {
-      if (t == 0) {
-        krange[0] = src_block((U + (double)(i0 + c0)) / dN);
-        krange[1] = src_block((U + (double)(i0 + c0 + cn - 1)) / dN);
+  for (int c0 = 0; c0 < n; c0 += FCH) {
+    const int cn = min(FCH, n - c0);
+    __syncthreads();  // the previous chunk has consumed xs
+    if (c0 > 0)  // own rows past the first flow round, from x_out
+      for (int e = t; e < FCH * XW; e += FB) {
+        const int j = e % FCH, d = e / FCH;
+        xs[j * XW + d] = (j < cn && d < NX) ? wt_load(p.f.x_out + (int64_t)d * Npad + i0 + c0 + j) : 0.0;
       }
-      __syncthreads();
-      const int klo = krange[0], nk = krange[1] - krange[0] + 1;
-      const bool staged = nk <= FNST;
-      if (staged)
-        for (int q2 = t; q2 < nk * FPPB; q2 += FB) {
-          const int kk = klo + q2 / FPPB, jj = q2 % FPPB;
-          const int64_t g = (int64_t)kk * p.ppb + jj;
-          slice[q2] = (jj < p.ppb && g < N) ? wt_load(p.cdf + g) : INFINITY;
-        }
-      __syncthreads();
-      if (t < cn) {
-        const double pos = (U + (double)(i0 + c0 + t)) / dN;
-        const int k = src_block(pos);
-        const int64_t g0 = (int64_t)k * p.ppb;
-        const int len = (int)min((int64_t)p.ppb, N - g0);
-        int lo = 0, hi = len;
-        if (staged && k >= klo && k < klo + nk) {
-          const double* cs = slice + (k - klo) * FPPB;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pos < cs[mid]) hi = mid; else lo = mid + 1;
-          }
+    for (int j = t; j < FCH; j += FB) {
+      double wj = 0.0;
+      if (j < cn) {
+        const int jg = c0 + j;
+        if (flag) {
+          const int64_t lo = jg == 0 ? slo0 : max(slo0, shi[jg - 1]);
+          wj = shi[jg] > lo ? (double)(shi[jg] - lo) / dN : 0.0;
         } else {
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pos < wt_load(p.cdf + g0 + mid)) hi = mid; else lo = mid + 1;
-          }
+          wj = (fb * lws[jg]) / S;
         }
-        anc[t] = (int)(g0 + (lo < len ? lo : len - 1));
       }
-      __syncthreads();
-    }
-    // rows: particle-fastest mapping (coalesced copy-through; gathered rows on a resample);
-    // all of a thread's loads are issued before any store so their latencies overlap
-    constexpr int RPT = (FMC * MB::XW + FB - 1) / FB;
-    double rv[RPT];
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int q2 = t + r * FB;
-      const int j = q2 % FMC, d = q2 / FMC;
-      rv[r] = 0.0;
-      if (q2 < FMC * MB::XW && j < cn && d < NX)
-        rv[r] = wt_load(p.f.x_out + (int64_t)d * Npad + (flag ? (int64_t)anc[j] : i0 + c0 + j));
-    }
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int q2 = t + r * FB;
-      const int j = q2 % FMC, d = q2 / FMC;
-      if (q2 < FMC * MB::XW) {
-        double v = 0.0;
-        if (j < cn && d < NX) {
-          wt_store(p.x_res + (int64_t)d * Npad + i0 + c0 + j, rv[r]);
-          v = rv[r] - p.shift[d];
-        }
-        xs[j * MB::XW + d] = v;
-      }
-    }
-    for (int j = t; j < FMC; j += FB) {
-      const double wj = j < cn ? (flag ? 1.0 / dN : (fb * lws[c0 + j]) / S) : 0.0;
       ws[j] = wj;
-      if (j < cn) p.w_out[i0 + c0 + j] = wj;
     }
     __syncthreads();
-    if (t <= NX) {
-      if (t == 0)
-        for (int j = 0; j < cn; ++j) a0acc += ws[j];
-      else
-        for (int j = 0; j < cn; ++j) a1acc += ws[j] * xs[j * MB::XW + t - 1];
-    }
     if (sl < MB::SL) {
+#pragma unroll 4
       for (int j = sl; j < cn; j += MB::SL) {
-        const double* r = xs + j * MB::XW;
+        const double* r = xs + j * XW;
         const double wj = ws[j];
         double u[4], v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          u[k] = r[4 * bi + k] * wj;
-          v[k] = r[4 * bj + k];
+          u[k] = (r[4 * bi + k] - shb_i[k]) * wj;
+          v[k] = r[4 * bj + k] - shb_j[k];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
           for (int l = 0; l < 4; ++l) acc[k * 4 + l] += u[k] * v[l];
+        if (diagp) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) a1[k] += u[k];
+          if (pair == 0) a0acc += wj;
+        }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   unsigned long long* cp = p.cpart + (int64_t)b * MM::E;
-  if (t <= NX) f_st(cp + t, t == 0 ? a0acc : a1acc);
-  if (sl < MB::SL)
+  __shared__ double s1red[MB::SL][MB::NB * 4 + 1];
+  if (sl < MB::SL) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) mred[sl][pair][k] = acc[k];
+    if (diagp)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s1red[sl][1 + 4 * bi + k] = a1[k];
+    if (pair == 0) s1red[sl][0] = a0acc;
+  }
   __syncthreads();
+  if (t <= NX) {  // W and S1 over the slices (fixed order)
+    double a = 0.0;
+    for (int s2 = 0; s2 < MB::SL; ++s2) a += s1red[s2][t];
+    f_st(cp + t, a);
+  }
   if (t < MB::NPAIR) {
     int ci = 0, rem = t;
     while (rem >= MB::NB - ci) { rem -= MB::NB - ci; ++ci; }
@@ -388,60 +559,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
         f_st(cp + 1 + NX + (d * NX - d * (d - 1) / 2 + (e - d)), a);
       }
   }
-  LF_STAMP(7);
-  if (!f_barrier(p, ph + 4)) return;
-  LF_STAMP(8);
-
-  // ---- P5: final reduction, 16 output entries per round, rounds strided over workgroups ----
-  constexpr int NOUT = NX + MM::NP;
-  __shared__ double fpart[4][FB / 16][17];
-  if (b == 0 && t == 0) {
-    p.stat[0] = ess;
-    p.stat[1] = flag ? 1.0 : 0.0;
-    p.stat[2] = S;
-    if (p.o_ess) *p.o_ess = ess;
-    if (p.o_flag) *p.o_flag = flag ? 1 : 0;
-  }
-  const int el = t / 16, pl = t % 16;
-  for (int g0 = b * (FB / 16); g0 < NOUT; g0 += p.nbk * (FB / 16)) {
-    const int qo = g0 + el;
-    const bool live = qo < NOUT;
-    int d = 0, e = 0;
-    if (live && qo >= NX) pair_of(qo - NX, NX, &d, &e);
-    const int src[4] = {0, 1 + (qo < NX ? qo : d), 1 + e, qo >= NX ? 1 + NX + (qo - NX) : 0};
-    double tot4[4] = {0.0, 0.0, 0.0, 0.0};
-    if (live)
-      for (int k = pl; k < p.nbk; k += 16) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) tot4[f] += f_ld(p.cpart + (int64_t)k * MM::E + src[f]);
-      }
-#pragma unroll
-    for (int f = 0; f < 4; ++f) fpart[f][el][pl] = tot4[f];
-    __syncthreads();
-    if (pl == 0 && live) {
-      double tot[4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        double sum = 0.0;
-        for (int k = 0; k < 16; ++k) sum += fpart[f][el][k];
-        tot[f] = sum;
-      }
-      const double sw = tot[0];
-      if (qo < NX) {
-        const double mv = p.shift[qo] + tot[1] / sw;
-        p.mean[qo] = mv;
-        if (p.o_mean) p.o_mean[qo] = mv;
-      } else {
-        const double c = tot[3] / sw - (tot[1] / sw) * (tot[2] / sw);
-        if (p.o_cov) {
-          p.o_cov[d * NX + e] = c;
-          p.o_cov[e * NX + d] = c;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  LF_STAMP(9);
+  LF_STAMP(5);
 }
 
 }  // namespace ledh

@@ -44,6 +44,21 @@
 namespace pf {
 namespace ledh {
 
+// diagnostic phase stamps (PF_STAMPS builds only): s_memrealtime (100 MHz) per workgroup, slots
+// 0-5 the fused step's phases (pf_ledh_fused.h), 6-11 the first flow round's sub-phases
+#ifdef PF_STAMPS
+constexpr int FST = 12;
+__device__ unsigned long long g_ledh_stamps[256 * FST];
+#define LF_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_ledh_stamps[blockIdx.x * FST + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LF_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 constexpr int TB = 256;    // block of the per-particle-thread and reduction kernels
 constexpr int LT = 1024;   // particles per reduction tile
 constexpr int MAXT = 1024; // tiles (N <= LT * MAXT)
@@ -540,16 +555,23 @@ __device__ __forceinline__ double group_sum(double v) {
 // eta0 = g(x_{k-1}, u) + v of particle i over a lane group (ledh.py:104-115): gx = g(x) and v
 // (PER components per lane, lane q of the group holds components q*PER ..)
 template <int NX, int NZ, int TK>
-__device__ __forceinline__ void group_prior(const FlowParams& p, const double* __restrict__ Pm, int64_t i, int q,
-                                            int base, double* gx, double* v) {
+// (src: the row of x_in the particle in slot i starts from - i itself, or its resampling ancestor
+// when the previous step's resample is applied here, k_ledh_fused)
+// (xpre: the lane's PER components of that row, already loaded by the caller, or null)
+__device__ __forceinline__ void group_prior(const FlowParams& p, const double* __restrict__ Pm, int64_t i, int64_t src,
+                                            int q, int base, double* gx, double* v, const double* xpre = nullptr) {
   using L = Lay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
   double x[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int a = q * PER + j;
-    x[j] = a < NX ? p.x_in[(int64_t)a * p.Npad + i] : 0.0;
+    x[j] = xpre ? xpre[j] : (a < NX ? p.x_in[(int64_t)a * p.Npad + src] : 0.0);
   }
+#ifdef PF_STAMPS
+  asm volatile("" ::"v"(x[0]));
+  LF_STAMP(6);
+#endif
   // ---- g(x_{k-1}, u) ------------------------------------------------------------
   if constexpr (TK == PF_TRANS_L96) {
     static_assert(NX % GL == 0 && PER >= 2, "L96 lane groups hold >= 2 contiguous components each");
@@ -582,6 +604,10 @@ __device__ __forceinline__ void group_prior(const FlowParams& p, const double* _
     const double h6 = dt / 6.0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) gx[j] = x[j] + h6 * (acc[j] + k[j]);
+#ifdef PF_STAMPS
+    asm volatile("" ::"v"(gx[PER - 1]));
+    LF_STAMP(7);
+#endif
   } else {
 #pragma unroll
     for (int j = 0; j < PER; ++j) gx[j] = 0.0;
@@ -662,18 +688,25 @@ __device__ __forceinline__ double wt_load(const double* p) {
       (long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// The affine flow of particle i by its lane group (lane q of GL): writes eta_L to x_out
-// (write-through when WT) and returns the unnormalised log weight (valid in every lane of the group).
+// The affine flow of particle i by its lane group (lane q of GL): eta_L -> eta[PER] (this lane's
+// components q*PER ..), returns the unnormalised log weight (valid in every lane of the group);
+// w_i = w_in[i], loaded by the caller ahead of the chain.
 // Pm: the parameter block (Lay), af: the composed flow (TLay::aff) - p.Pm / p.table in HBM, or
 // copies staged in LDS (k_ledh_fused).
-template <int NX, int NZ, int TK, bool WT = false>
+template <int NX, int NZ, int TK>
 __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
-                                                      const double* __restrict__ af, int64_t i, int q, int base) {
+                                                      const double* __restrict__ af, int64_t i, int64_t src, int q,
+                                                      int base, double* eta, double w_i,
+                                                      const double* xpre = nullptr) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
   double gx[PER], v[PER];
-  group_prior<NX, NZ, TK>(p, Pm, i, q, base, gx, v);
+  group_prior<NX, NZ, TK>(p, Pm, i, src, q, base, gx, v, xpre);
+#ifdef PF_STAMPS
+  asm volatile("" ::"v"(v[PER - 1]), "v"(gx[PER - 1]));
+  LF_STAMP(8);
+#endif
   // ---- eta0, y0 = H eta0 (group all-reduce), the composed flow ----------------------
   double e0[PER];
 #pragma unroll
@@ -689,6 +722,10 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
     }
     y0[k] = group_sum<GL>(acc);
   }
+#ifdef PF_STAMPS
+  asm volatile("" ::"v"(y0[NZ - 1]));
+  LF_STAMP(9);
+#endif
   double dd[PER];  // eta - g(x) = v + delta
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -697,14 +734,18 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
       double acc = af[T::D0 + a];
 #pragma unroll
       for (int k = 0; k < NZ; ++k) acc += af[T::DM + a * NZ + k] * y0[k];
-      if constexpr (WT) wt_store(p.x_out + (int64_t)a * p.Npad + i, e0[j] + acc);
-      else p.x_out[(int64_t)a * p.Npad + i] = e0[j] + acc;
+      eta[j] = e0[j] + acc;
       dd[j] = v[j] + acc;
     } else {
+      eta[j] = 0.0;
       dd[j] = 0.0;
     }
   }
   // ---- log weight (ledh.py:186-190) -----------------------------------------------
+#ifdef PF_STAMPS
+  asm volatile("" ::"v"(dd[PER - 1]));
+  LF_STAMP(10);
+#endif
   const double part = group_trans_part<NX, NZ>(p, Pm, q, base, dd, v);
   double ez[NZ];
 #pragma unroll
@@ -715,7 +756,7 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
     ez[k] = p.z[k] - (yl + Pm[L::C + k]);
   }
   const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
-  return (log(p.w_in[i] + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
+  return (log(w_i + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
 }
 
 template <int NX, int NZ, int TK>
@@ -726,7 +767,13 @@ __global__ void __launch_bounds__(TB) k_flow_affine(FlowParams p) {
   if (i >= p.N) return;  // whole groups leave together
   const int q = (int)(tid % GL);
   const int base = (threadIdx.x & 63) - q;
-  const double l = flow_affine_particle<NX, NZ, TK>(p, p.Pm, p.table + TLay<NX, NZ>::aff(p.L), i, q, base);
+  constexpr int PER = Grp<NX>::PER;
+  double eta[PER];
+  const double l =
+      flow_affine_particle<NX, NZ, TK>(p, p.Pm, p.table + TLay<NX, NZ>::aff(p.L), i, i, q, base, eta, p.w_in[i]);
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (q * PER + j < NX) p.x_out[(int64_t)(q * PER + j) * p.Npad + i] = eta[j];
   if (q == 0) p.lw[i] = l;
 }
 

@@ -90,7 +90,7 @@ __device__ __forceinline__ void grp_rows(const Real* loc, const Real* __restrict
 template <typename Real, int NX, bool LOCAL>
 __device__ __forceinline__ void grp_add_lower(Real* x, const Real* n, const Real* __restrict__ P, int off, int q,
                                               int base) {
-  constexpr int PER = SGrp<NX>::PER, SGL = SGrp<NX>::GL;
+  constexpr int PER = SGrp<NX>::PER;
   Real acc[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) acc[j] = Real(0);
