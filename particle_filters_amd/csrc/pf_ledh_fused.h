@@ -218,6 +218,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   __shared__ double mred[MB::SL][MB::NPAIR][16];
   __shared__ double pms[L::SIZE];     // the parameter block (the parts the flow reads)
   __shared__ double afs[TL::AFF_SIZE];  // the composed flow
+  __shared__ double zs[NZ];             // the step's observation
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t N = p.f.N, Npad = p.f.Npad;
   const int64_t i0 = (int64_t)b * p.ppb;
@@ -304,6 +305,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       }
     }
   }
+  if (t < NZ) zs[t] = p.f.z[t];
   if (p.p5) {  // the previous step's outputs and mean (= this step's shift)
     p5_0.finish(p, v5);
     for (int r = 1; r < P5<NX, FB>::rounds(p); ++r) {
@@ -328,7 +330,8 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       const int64_t src = c0 == 0 ? src1 : (p.anc_in ? (int64_t)p.anc_in[i] : i);
       const double wi = c0 == 0 ? w1 : p.f.w_in[i];
       double eta[PER];
-      const double l = flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, c0 == 0 ? x1 : nullptr);
+      const double l =
+          flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, c0 == 0 ? x1 : nullptr, zs);
 #ifdef PF_STAMPS
       asm volatile("" ::"v"(l));
       if (c0 == 0) LF_STAMP(11);

@@ -520,7 +520,9 @@ __global__ void __launch_bounds__(SB) k_compose(double* table, const double* lam
 // ---------------------------------------------------------------------------
 template <int NX>
 struct Grp {
-  static constexpr int GL = NX >= 16 ? 4 : 1;  // lanes per particle
+  // lanes per particle (8 for L96 d = 40 was tried: inside k_ledh_fused it needs ~540 registers
+  // against the 256 of two waves per SIMD and spilled ~290 VGPRs to scratch)
+  static constexpr int GL = NX >= 16 ? 4 : 1;
   static constexpr int PER = (NX + GL - 1) / GL;
 };
 
@@ -697,7 +699,7 @@ template <int NX, int NZ, int TK>
 __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
                                                       const double* __restrict__ af, int64_t i, int64_t src, int q,
                                                       int base, double* eta, double w_i,
-                                                      const double* xpre = nullptr) {
+                                                      const double* xpre = nullptr, const double* zz = nullptr) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
@@ -747,13 +749,14 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
   LF_STAMP(10);
 #endif
   const double part = group_trans_part<NX, NZ>(p, Pm, q, base, dd, v);
+  const double* __restrict__ z = zz ? zz : p.z;
   double ez[NZ];
 #pragma unroll
   for (int k = 0; k < NZ; ++k) {
     double yl = af[T::PL + k];
 #pragma unroll
     for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
-    ez[k] = p.z[k] - (yl + Pm[L::C + k]);
+    ez[k] = z[k] - (yl + Pm[L::C + k]);
   }
   const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
   return (log(w_i + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
