@@ -85,6 +85,32 @@ __device__ __forceinline__ double f_ld(const unsigned long long* p) {
 __device__ __forceinline__ void f_std(double* p, double v) { f_st((unsigned long long*)p, v); }
 __device__ __forceinline__ double f_ldd(const double* p) { return f_ld((const unsigned long long*)p); }
 
+// Block reductions with the wave step on the DPP network (a fixed tree: the same result in every
+// workgroup); an LDS-only barrier variant (s_waitcnt lgkmcnt(0) + s_barrier instead of
+// __syncthreads' vmcnt(0) wait for the write-through stores) was measured: no change.
+__device__ __forceinline__ double dpp_reduce_sum(double v, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum_ud(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += red[k];
+  __syncthreads();
+  return s;
+}
+__device__ __forceinline__ double dpp_reduce_max(double v, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max_ud(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = red[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) s = fmax(s, red[k]);
+  __syncthreads();
+  return s;
+}
+
 // grid barrier: every workgroup publishes `phase` in its word, then waits for all words >= phase.
 // False on timeout (the launch is abandoned and *err set; the host reports it).
 __device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long long phase) {
@@ -354,7 +380,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       }
     }
   }
-  m = block_reduce_max(m, red);
+  m = dpp_reduce_max(m, red);
 
   // ---- P2: exponentials relative to the WORKGROUP max, sums and scan (no grid max needed:
   //      the workgroups' (max, sum, sum of squares) combine exactly after one barrier) ----------
@@ -369,7 +395,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     s2 += e * e;
   }
   {
-    const double inc = wave_incl_scan64(s1, lane);
+    const double inc = wave_incl_scan_dpp(s1);
     if (lane == 63) red[wv] = inc;
     __syncthreads();
     double off = 0.0;
@@ -381,8 +407,8 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     }
     __syncthreads();
   }
-  const double S_b = block_reduce_sum(s1, red);
-  const double S2_b = block_reduce_sum(s2, red);
+  const double S_b = dpp_reduce_sum(s1, red);
+  const double S2_b = dpp_reduce_sum(s2, red);
   if (t == 0) {
     f_st(p.part + 0 * FMAX + b, m);
     f_st(p.part + 1 * FMAX + b, S_b);
@@ -401,11 +427,11 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     s2k = f_ld(p.part + 2 * FMAX + t);
     slk = f_ld(p.part + 3 * FMAX + t);
   }
-  const double M = block_reduce_max(sk > 0.0 ? mk : -INFINITY, red);
+  const double M = dpp_reduce_max(sk > 0.0 ? mk : -INFINITY, red);
   const double fk = (sk > 0.0) ? exp(mk - M) : 0.0;
   {
     const double v = sk * fk;
-    const double inc = wave_incl_scan64(v, lane);
+    const double inc = wave_incl_scan_dpp(v);
     if (lane == 63) red[wv] = inc;
     __syncthreads();
     double off = 0.0;
@@ -421,7 +447,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   const double S = boff[FMAX];
   const double fb = red[8];
   const double lastprev = b > 0 ? red[9] : -INFINITY;
-  const double E2 = block_reduce_sum(s2k * fk * fk, red);
+  const double E2 = dpp_reduce_sum(s2k * fk * fk, red);
   const double ess = 1.0 / (E2 / (S * S));
   const bool flag = (p.ratio > 0.0) && (ess < p.ratio * (double)N);
   if (b == 0 && t == 0) {

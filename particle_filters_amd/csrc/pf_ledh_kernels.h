@@ -39,6 +39,7 @@
 #include <stdint.h>
 
 #include "../../include/pf_ledh.h"
+#include "pf_dpp.h"
 #include "philox.h"
 
 namespace pf {
@@ -549,6 +550,7 @@ __device__ __forceinline__ void group_rows(const double* loc, const double* __re
 
 template <int GL>
 __device__ __forceinline__ double group_sum(double v) {
+  if constexpr (GL == 4) return quad_sum_d(v);  // xor 1, xor 2 on the DPP network: the same sums
 #pragma unroll
   for (int o = 1; o < GL; o <<= 1) v += __shfl_xor(v, o);
   return v;
@@ -581,9 +583,20 @@ __device__ __forceinline__ void group_prior(const FlowParams& p, const double* _
     const int nxt = base + (q + 1) % GL, prv = base + (q + GL - 1) % GL;
     auto rhs = [&](const double* y, double* k) {
       // neighbours across the lane boundary: y[a+1] from the next lane, y[a-1], y[a-2] from the previous
-      const double nx0 = GL == 1 ? y[0] : __shfl(y[0], nxt);
-      const double pv1 = GL == 1 ? y[PER - 1] : __shfl(y[PER - 1], prv);
-      const double pv2 = GL == 1 ? y[PER - 2] : __shfl(y[PER - 2], prv);
+      double nx0, pv1, pv2;
+      if constexpr (GL == 1) {
+        nx0 = y[0];
+        pv1 = y[PER - 1];
+        pv2 = y[PER - 2];
+      } else if constexpr (GL == 4) {  // quad rotations on the DPP network (no LDS crossbar)
+        nx0 = dpp_d<DPP_QP_ROT1>(0.0, y[0]);
+        pv1 = dpp_d<DPP_QP_ROT3>(0.0, y[PER - 1]);
+        pv2 = dpp_d<DPP_QP_ROT3>(0.0, y[PER - 2]);
+      } else {
+        nx0 = __shfl(y[0], nxt);
+        pv1 = __shfl(y[PER - 1], prv);
+        pv2 = __shfl(y[PER - 2], prv);
+      }
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         const double yp1 = j + 1 < PER ? y[j + 1] : nx0;

@@ -604,14 +604,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   auto body = [&, p](auto out_tag) {  // p by value: its fields stay in registers, not kernarg reloads
   constexpr bool outwg = decltype(out_tag)::value;  // b == G - 1
   // ---- entry state (k_step layout) and its normaliser ------------------------
-  // the first observation window (NZ == 1: lane k holds z of step k) is loaded before the state,
-  // so its latency overlaps the state's instead of following it at the first step
-  float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
-  int64_t zbase = -64;
-  if (NZ == 1 && p.T > 0) {
-    zbase = 0;
-    zwin = lane < p.T ? p.z[(size_t)lane * R + r] : 0.0f;
-  }
   float x[RPPT], l[RPPT];
   double F0 = 0.0, T0 = 0.0;  // entry frame and absolute log mass (from the entry header)
   {
@@ -695,6 +687,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   double Tlast = T0;    // absolute log mass of the last verified (not resampled) step
   int last_cur = 0;     // mslot buffer of the last computed step, and its frame
   double F_last = F0;
+  float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
+  int64_t zbase = -64;
   while (alive) {
     // granules of the step this iteration verifies (waves 0..RCW-1: one record per lane); per
     // iteration, so they are not carried around the loop (and through the rollback) in VGPRs.
