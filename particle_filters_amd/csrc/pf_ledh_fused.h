@@ -203,10 +203,15 @@ struct P5 {
       if (k0 + P5K * lpe >= p.nbk) break;
       load(p, k0 + P5K * lpe, v);
     }
+    // the group sum on the DPP network: 16-lane rows, then rows 0+1 / 2+3 into lanes 31 / 63, then
+    // the whole wave into lane 63 (a fixed tree; the group's last lane holds its sum)
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
-      for (int o = 1; o < lpe; o <<= 1) tot[f] += __shfl_xor(tot[f], o);
-    if (live && gl == 0) {
+    for (int f = 0; f < 4; ++f) {
+      tot[f] = row_sum_d(tot[f]);
+      if (lpe >= 32) tot[f] += dpp_d<DPP_ROW_BCAST15, 0xa>(0.0, tot[f]);
+      if (lpe == 64) tot[f] += dpp_d<DPP_ROW_BCAST31, 0xc>(0.0, tot[f]);
+    }
+    if (live && gl == lpe - 1) {
       const double sw = tot[0];
       if (qo < NX) {
         const double mv = p.shift5[qo] + tot[1] / sw;
@@ -420,6 +425,21 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   LF_STAMP(3);
 
   // ---- P3: global normaliser, ESS, decision; this slice of the CDF; the ancestors -----------
+  // P4's moment shift is loaded here with the partials: one round trip for both
+  const int pair = t % MB::NPAIR, sl = t / MB::NPAIR;
+  int bi = 0, bj = 0;
+  {
+    int rem = pair;
+    while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
+    bj = bi + rem;
+  }
+  double shb_i[4], shb_j[4];  // the shift of this thread's two 4-blocks (written by P5' of other
+                              // workgroups this launch: write-through loads after B1)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    shb_i[k] = 4 * bi + k < NX ? f_ldd(p.shift + 4 * bi + k) : 0.0;
+    shb_j[k] = 4 * bj + k < NX ? f_ldd(p.shift + 4 * bj + k) : 0.0;
+  }
   double mk = -INFINITY, sk = 0.0, s2k = 0.0, slk = 0.0;
   if (t < p.nbk) {
     mk = f_ld(p.part + 0 * FMAX + t);
@@ -494,20 +514,6 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   // ---- P4: moment partials of the reported set from the own rows --------------------------
   // after a resample particle j stands for its n_j slots (weight n_j / N): the same sums as over
   // the post-resample slots; otherwise its normalised weight
-  const int pair = t % MB::NPAIR, sl = t / MB::NPAIR;
-  int bi = 0, bj = 0;
-  {
-    int rem = pair;
-    while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
-    bj = bi + rem;
-  }
-  double shb_i[4], shb_j[4];  // the shift of this thread's two 4-blocks (written by P5' of other
-                              // workgroups this launch: write-through loads after B1)
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    shb_i[k] = 4 * bi + k < NX ? f_ldd(p.shift + 4 * bi + k) : 0.0;
-    shb_j[k] = 4 * bj + k < NX ? f_ldd(p.shift + 4 * bj + k) : 0.0;
-  }
   double a0acc = 0.0, a1[4] = {0.0, 0.0, 0.0, 0.0};  // W (pair 0), S1 of block bi (diagonal pairs)
   const bool diagp = bi == bj;
   double acc[16];
