@@ -533,7 +533,6 @@ template <typename Real, int NX, int NZ, int TK, int OK>
 __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   static_assert(NX == 1 && sizeof(Real) == 4, "resident path: scalar fp32 state");
   using Mo = Model<Real, NX, NZ, TK, OK>;
-  using WA = WAcc<Real, NX>;
   using RC = Rec<NX>;
   constexpr int LAG = RLAG;
   constexpr int NSNAP = LAG + 1;
