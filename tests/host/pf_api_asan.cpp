@@ -68,8 +68,11 @@ static void error_paths() {
   bad.nx = 0;
   CHECK(pf_create(&bad, &o, &h) != PF_OK && h == nullptr);
   bad = m;
-  bad.n_trans_params = 3;  // A must be nx*nx
-  CHECK(pf_create(&bad, &o, &h) != PF_OK && h == nullptr);
+  bad.n_trans_params = 0;  // A needs at least nx*nx values
+  CHECK(pf_create(&bad, &o, &h) == PF_E_ARG && h == nullptr);
+  bad = m;
+  bad.n_obs_params = 0;  // beta needs at least nz values
+  CHECK(pf_create(&bad, &o, &h) == PF_E_ARG && h == nullptr);
   pf_opts bo = o;
   bo.n_particles = 0;
   CHECK(pf_create(&m, &bo, &h) != PF_OK && h == nullptr);

@@ -35,8 +35,6 @@ def test_host_asan_error_paths_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(os.environ.get("PF_ASAN_GPU") != "1",
-                    reason="host-ASan GPU leg not yet run on the MI355X pool; PF_ASAN_GPU=1 runs it")
 def test_host_asan_filter_runs_gpu():
     assert os.path.exists(EXE), "build/pf_api_asan missing: run __graft_entry__.build() (make asan) first"
     r = _run(300)
