@@ -54,7 +54,12 @@ pf_status pf_edh_step(pf_ledh_handle* h, const double* P, const double* xbar, co
 
 /* The whole T loop on the device with no host synchronisation inside T: Ps [T][nx][nx] tracker
  * covariances, Xbars [T][nx] the tracker's past means, Z [T][nz], U [T][nx] or NULL.  Noise
- * PF_NOISE_NONE or PF_NOISE_DEVICE; resampling uniforms from Philox.  Outputs as pf_ledh_run. */
+ * PF_NOISE_NONE, PF_NOISE_DEVICE (resampling uniforms from Philox) or PF_NOISE_HOST: the replayed
+ * draws set by pf_ledh_set_run_replay for a run of exactly this T — step t's process noise V_t
+ * [N][nx] and resampling uniform U_t, where U_t is read only on steps that resample, so the caller
+ * lays the uniforms out with the decisions it expects and checks the returned flags against them.
+ * A failed launch or grid-barrier timeout inside the run leaves the handle uninitialised
+ * (PF_E_NOT_INITIALIZED on the next call).  Outputs as pf_ledh_run. */
 pf_status pf_edh_run(pf_ledh_handle* h, const double* Ps, const double* Xbars, const double* Z, const double* U,
                      int64_t T, int32_t noise, double* means, double* covs, double* ess, uint8_t* flags);
 

@@ -140,7 +140,8 @@ pf_status pf_resample_state(pf_handle* h, const double* uniforms, const double* 
  * when first_update_only (notebook driver, PF_VS_experiments.ipynb cell 7) — with no
  * host synchronisation inside T.  Z [T][R][nz]; U [T][R][nx] or NULL.
  * Outputs (host, nullable): means [T][R][nx] (post-resample when resampled, as the
- * reference's PFState.mean), covs [T][R][nx][nx] (nx <= 4), neff [T][R] (pre-resample),
+ * reference's PFState.mean), covs [T][R][nx][nx] (any nx: the step records carry them for nx <= 4,
+ * the device-loop covariance kernels of pf_cov.h for larger states), neff [T][R] (pre-resample),
  * flags [T][R], log_norm [T][R]. */
 pf_status pf_run(pf_handle* h, const double* Z, const double* U, int64_t T, int32_t first_update_only,
                  double* means, double* covs, double* neff, uint8_t* flags, double* log_norm);
@@ -211,6 +212,16 @@ int32_t pf_last_run_resident(pf_handle* h);
  * pf_last_run_ms waits for the last run and returns the device time between them. */
 pf_status pf_set_timing(pf_handle* h, int32_t on);
 pf_status pf_last_run_ms(pf_handle* h, float* ms);
+/* Verification trace of the register-resident kernel (tests; the shipped kernel instance is not
+ * touched: a second instance with the trace stores runs while a trace is set).  pf_set_trace
+ * allocates room for T_cap steps (0 frees it).  While set, every resident run records, for each
+ * of its first T_cap steps, the state its verification accepted - after any rollback and
+ * recomputation inside the launch: the predicted particles and pre-resample log-weights (fp32,
+ * any uniform frame), and on a resample step the ancestor index of every output slot (-1
+ * elsewhere).  pf_get_trace copies step t (of the last run) of replicate r: x, l, anc [N]
+ * (nullable), and resets that step's ancestors to -1. */
+pf_status pf_set_trace(pf_handle* h, int64_t T_cap);
+pf_status pf_get_trace(pf_handle* h, int64_t t, int32_t r, float* x, float* l, int32_t* anc);
 /* Geometry of the step launch: tiles per replicate, tile size, dynamic LDS bytes. */
 pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds_bytes);
 

@@ -85,7 +85,9 @@ pf_status pf_ledh_set_state(pf_ledh_handle* h, const double* particles, const do
  * Ps [T][nx][nx] tracker covariances, Z [T][nz], U [T][nx] or NULL.  Noise PF_NOISE_NONE,
  * PF_NOISE_DEVICE (resampling uniforms from Philox) or PF_NOISE_HOST (the draws set by
  * pf_ledh_set_run_replay for a run of this T).  Outputs (host, nullable): means [T][nx],
- * covs [T][nx][nx], ess [T], flags [T]. */
+ * covs [T][nx][nx], ess [T], flags [T].  A failed launch or grid-barrier timeout inside the run
+ * leaves the handle uninitialised (PF_E_NOT_INITIALIZED on the next call): its state would be
+ * part-advanced. */
 pf_status pf_ledh_run(pf_ledh_handle* h, const double* Ps, const double* Z, const double* U, int64_t T,
                       int32_t noise, double* means, double* covs, double* ess, uint8_t* flags);
 

@@ -289,3 +289,220 @@ done:
   free(bmax);
   return status;
 }
+
+/*
+ * One step of the filter from a given state, compared with an engine's record of the same
+ * step (the verification trace of the register-resident kernel, include/pf_engine.h
+ * pf_get_trace).  Oracle side: pf.py:223-269 + _resample pf.py:188-220 in fp64 on the
+ * engine's Philox draws (predict epoch c->epoch, resample epoch c->epoch + 1), started from
+ * x0 / w0 (the engine's state before the step, w0 normalised).  Engine side: xe [N] predicted
+ * particles, le [N] pre-resample log-weights (fp32, any uniform frame), anc [N] the ancestor of
+ * every slot when the engine resampled (NULL otherwise), and the step's reported Neff / flag /
+ * mean / variance (post-resample moments when it resampled, pf.py:266-267).  Every quantity of
+ * c's "measured" block is filled in; the tolerances are the caller's.  Returns 0, -1 when an
+ * allocation failed.
+ */
+typedef struct pfo_step_check {
+  /* in */
+  int64_t N;
+  uint64_t seed;
+  uint32_t rep, epoch;
+  double thresh;
+  int32_t bm24, regularize;
+  double u;  /* control input of the step (0: none) */
+  double z;
+  double neff_e, mean_e, var_e;
+  int32_t flag_e, _pad0;
+  /* measured */
+  double dx_pre;       /* max |xe - x_oracle| after predict */
+  double mean_abs_x;   /* E_w |x_oracle| (scale of the state) */
+  double tv_w;         /* total-variation distance of the normalised weights */
+  double dcdf;         /* max |cdf_e - cdf_o| (fp64 cumsums of both weight sets) */
+  double lmag;         /* E_w |log-likelihood| (oracle weights) */
+  double eps_w;        /* E_w of the per-particle fp32 rounding bound of the engine's weights */
+  double neff_o, neff_rel;
+  int32_t flag_o, near_threshold;
+  double U;            /* systematic uniform of the step */
+  int64_t n_anc_bad;   /* slots with an ancestor out of range / unwritten / not monotone */
+  int64_t n_anc_self_diff, n_anc_oracle_diff;
+  double max_margin_self, max_margin_oracle;  /* distance of a differing slot's position to its
+                                                 ancestor's interval (engine's own / oracle CDF) */
+  double dmean, dvar;  /* engine mean / variance vs the oracle's set under the engine's decision
+                          (and ancestors) */
+  double dmean_oracle; /* vs the oracle's own ancestors */
+  double mean_o, var_o;
+} pfo_step_check;
+
+static double dll_dz(const pfo_scalar_model* m, double x, double z) {
+  if (m->obs == 3) return -z * exp(-x) / (m->hc * m->hc);
+  const double hp = m->obs == 0 ? m->hH * x + m->hc : m->hc * exp(0.5 * x);
+  return -(z - hp) / (m->lr * m->lr);
+}
+
+static double dll_dx(const pfo_scalar_model* m, double x, double z) {
+  if (m->obs == 3) {
+    const double b2 = m->hc * m->hc;
+    return -0.5 * (1.0 - z * z * exp(-x) / b2);
+  }
+  const double hp = m->obs == 0 ? m->hH * x + m->hc : m->hc * exp(0.5 * x);
+  const double dh = m->obs == 0 ? m->hH : 0.5 * hp;
+  return (z - hp) / (m->lr * m->lr) * dh;
+}
+
+/* distance of pos to the interval [lo, hi) of ancestor a in cdf (0 inside) */
+static double interval_dist(const double* cdf, int64_t a, double pos) {
+  const double lo = a > 0 ? cdf[a - 1] : 0.0, hi = cdf[a];
+  if (pos < lo) return lo - pos;
+  if (pos >= hi) return pos - hi;
+  return 0.0;
+}
+
+int pfo_sir_scalar_check_step(const pfo_scalar_model* m, pfo_step_check* c, const double* x0, const double* w0,
+                              const float* xe, const float* le, const int32_t* anc) {
+  const int64_t N = c->N;
+  double* xo = (double*)malloc((size_t)N * sizeof(double));
+  double* wo = (double*)malloc((size_t)N * sizeof(double));
+  double* we = (double*)malloc((size_t)N * sizeof(double));
+  double* tmp = (double*)malloc((size_t)N * sizeof(double));
+  double* ll = (double*)malloc((size_t)N * sizeof(double));
+  if (!xo || !wo || !we || !tmp || !ll) {
+    free(xo); free(wo); free(we); free(tmp); free(ll);
+    return -1;
+  }
+  /* predict (pf.py:232-237) */
+  pfo_normals(c->seed, N, c->rep, c->epoch, 2u, c->bm24, tmp);
+  double dx = 0.0;
+  for (int64_t i = 0; i < N; ++i) {
+    xo[i] = (m->a * x0[i] + c->u) + tmp[i] * m->lq;
+    const double d = fabs((double)xe[i] - xo[i]);
+    if (d > dx || isnan(d)) dx = d;
+  }
+  c->dx_pre = dx;
+  /* update (pf.py:253-262) and the engine's weights from its own log-weights (fp64 softmax) */
+  double mo = -INFINITY, me = -INFINITY;
+  for (int64_t i = 0; i < N; ++i) {
+    ll[i] = -0.5 * quad_of(m, xo[i], c->z);
+    wo[i] = log(w0[i] + 1e-300) + ll[i];
+    if (wo[i] > mo) mo = wo[i];
+    if ((double)le[i] > me) me = (double)le[i];
+  }
+  double so = 0.0, se = 0.0;
+  for (int64_t i = 0; i < N; ++i) {
+    wo[i] = exp(wo[i] - mo);
+    so += wo[i];
+    we[i] = (le[i] > -INFINITY) ? exp((double)le[i] - me) : 0.0;
+    se += we[i];
+  }
+  double tv = 0.0, w2 = 0.0, lmag = 0.0, eps = 0.0, ax = 0.0, co = 0.0, ce = 0.0, dcdf = 0.0;
+  for (int64_t i = 0; i < N; ++i) {
+    wo[i] /= so;
+    we[i] /= se;
+    tv += fabs(we[i] - wo[i]);
+    w2 += wo[i] * wo[i];
+    lmag += wo[i] * fabs(ll[i]);
+    ax += wo[i] * fabs(xo[i]);
+    /* the fp32 rounding bound of the engine's log-weight of particle i: 8 fp32 half-ulps (2^-21
+       relative) of the log-weight and log-likelihood it is built from (the carried log-weight's
+       shift, the likelihood's few fp32 operations, the add), the fp32 observation carried through
+       the likelihood's slope in z, and the predicted particle's own rounding carried through its
+       slope in x */
+    const double ep = ldexp(1.0 + fabs((double)le[i]) + fabs(ll[i]), -21) +
+                      ldexp(fabs(dll_dz(m, xo[i], c->z)) * fabs(c->z), -23) +
+                      fabs(dll_dx(m, xo[i], c->z)) * fabs((double)xe[i] - xo[i]);
+    eps += wo[i] * ep;
+    co += wo[i];
+    ce += we[i];
+    const double d = fabs(ce - co);
+    if (d > dcdf) dcdf = d;
+  }
+  c->tv_w = 0.5 * tv;
+  c->dcdf = dcdf;
+  c->lmag = lmag;
+  c->eps_w = eps;
+  c->mean_abs_x = ax;
+  c->neff_o = 1.0 / w2;
+  c->neff_rel = fabs(c->neff_e / c->neff_o - 1.0);
+  c->flag_o = c->neff_o < c->thresh * (double)N;
+  c->near_threshold = fabs(c->neff_o - c->thresh * (double)N) / (double)N < 1e-3;
+  c->n_anc_bad = c->n_anc_self_diff = c->n_anc_oracle_diff = 0;
+  c->max_margin_self = c->max_margin_oracle = 0.0;
+  c->U = pfo_uniform53(c->seed, 0, c->rep, c->epoch + 1u);
+  if (c->flag_e && anc) {
+    /* the post-resample set under the engine's ancestors (+ the jitter, pf.py:212-218) */
+    double* cdf_o = tmp;
+    double* cdf_s = ll;
+    double a = 0.0, b = 0.0;
+    for (int64_t i = 0; i < N; ++i) {
+      a += wo[i];
+      cdf_o[i] = a;
+      b += we[i];
+      cdf_s[i] = b;
+    }
+    cdf_o[N - 1] = 1.0;
+    cdf_s[N - 1] = 1.0;
+    double* jit = NULL;
+    if (c->regularize) {
+      jit = (double*)malloc((size_t)N * sizeof(double));
+      if (!jit) {
+        free(xo); free(wo); free(we); free(tmp); free(ll);
+        return -1;
+      }
+      pfo_normals(c->seed, N, c->rep, c->epoch + 1u, 3u, c->bm24, jit);
+    }
+    double sf = 0.0, so2 = 0.0;
+    int64_t jo = 0, js = 0, prev = 0;
+    for (int64_t i = 0; i < N; ++i) {
+      const double pos = (c->U + (double)i) / (double)N;
+      while (jo < N - 1 && !(pos < cdf_o[jo])) ++jo; /* searchsorted(cdf, pos, 'right') */
+      while (js < N - 1 && !(pos < cdf_s[js])) ++js;
+      int64_t ai = anc[i];
+      if (ai < 0 || ai >= N || ai < prev) {
+        ++c->n_anc_bad;
+        ai = jo;
+      } else {
+        prev = ai;
+      }
+      if (ai != js) {
+        ++c->n_anc_self_diff;
+        const double d = interval_dist(cdf_s, ai, pos);
+        if (d > c->max_margin_self) c->max_margin_self = d;
+      }
+      if (ai != jo) {
+        ++c->n_anc_oracle_diff;
+        const double d = interval_dist(cdf_o, ai, pos);
+        if (d > c->max_margin_oracle) c->max_margin_oracle = d;
+      }
+      const double j = jit ? jit[i] * m->lj : 0.0;
+      sf += xo[ai] + j;
+      so2 += xo[jo] + j;
+      we[i] = xo[ai] + j; /* reuse: the forced set */
+    }
+    const double mf = sf / (double)N;
+    double vf = 0.0;
+    for (int64_t i = 0; i < N; ++i) vf += (we[i] - mf) * (we[i] - mf);
+    vf /= (double)N;
+    c->mean_o = mf;
+    c->var_o = vf;
+    c->dmean = fabs(c->mean_e - mf);
+    c->dvar = fabs(c->var_e - vf);
+    c->dmean_oracle = fabs(c->mean_e - so2 / (double)N);
+    free(jit);
+  } else {
+    /* no resample on the engine's side: the weighted predicted set (pf.py:266-267) */
+    double sw = 0.0, sx = 0.0;
+    for (int64_t i = 0; i < N; ++i) {
+      sw += wo[i];
+      sx += wo[i] * xo[i];
+    }
+    const double mean = sx / sw;
+    double v = 0.0;
+    for (int64_t i = 0; i < N; ++i) v += wo[i] * (xo[i] - mean) * (xo[i] - mean);
+    v /= sw;
+    c->mean_o = mean;
+    c->var_o = v;
+    c->dmean = c->dmean_oracle = fabs(c->mean_e - mean);
+    c->dvar = fabs(c->var_e - v);
+  }
+  free(xo); free(wo); free(we); free(tmp); free(ll);
+  return 0;
+}

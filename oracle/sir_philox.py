@@ -127,6 +127,20 @@ class _Opts(C.Structure):
                 ("mean0", C.c_double), ("var0", C.c_double)]
 
 
+class _StepCheck(C.Structure):
+    _fields_ = [("N", C.c_int64), ("seed", C.c_uint64), ("rep", C.c_uint32), ("epoch", C.c_uint32),
+                ("thresh", C.c_double), ("bm24", C.c_int32), ("regularize", C.c_int32), ("u", C.c_double),
+                ("z", C.c_double), ("neff_e", C.c_double), ("mean_e", C.c_double), ("var_e", C.c_double),
+                ("flag_e", C.c_int32), ("_pad0", C.c_int32),
+                ("dx_pre", C.c_double), ("mean_abs_x", C.c_double), ("tv_w", C.c_double), ("dcdf", C.c_double),
+                ("lmag", C.c_double), ("eps_w", C.c_double), ("neff_o", C.c_double), ("neff_rel", C.c_double),
+                ("flag_o", C.c_int32), ("near_threshold", C.c_int32), ("U", C.c_double),
+                ("n_anc_bad", C.c_int64), ("n_anc_self_diff", C.c_int64), ("n_anc_oracle_diff", C.c_int64),
+                ("max_margin_self", C.c_double), ("max_margin_oracle", C.c_double),
+                ("dmean", C.c_double), ("dvar", C.c_double), ("dmean_oracle", C.c_double),
+                ("mean_o", C.c_double), ("var_o", C.c_double)]
+
+
 _lib = None
 
 
@@ -150,6 +164,9 @@ def load():
         lib.pfo_normals.argtypes = [C.c_uint64, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, d]
         lib.pfo_uniform53.restype = C.c_double
         lib.pfo_uniform53.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.pfo_sir_scalar_check_step.restype = C.c_int
+        lib.pfo_sir_scalar_check_step.argtypes = [C.POINTER(_Model), C.POINTER(_StepCheck), d, d,
+                                                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int32)]
         lib.pfo_philox4x32_10.restype = None
         lib.pfo_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         _lib = lib
@@ -219,4 +236,29 @@ def run_scalar(model: _Model, Z, *, N, seed, rep=0, ep0=2, thresh=0.5, method="s
     out["dead_step"] = int(st) - 1 if st > 0 else -1
     out["flags"] = out["flags"].astype(bool)
     out["x"], out["w"] = x, w
+    return out
+
+
+def check_step(model: _Model, *, seed, rep, epoch, thresh, x0, w0, z, xe, le, anc, neff_e, flag_e, mean_e, var_e,
+               bm24=True, regularize=False, u=0.0) -> dict:
+    """One oracle step from the state (x0, w0) against an engine's record of the same step
+    (``pfo_sir_scalar_check_step`` in sir_philox.c): returns the measured quantities as a dict.
+    ``anc`` is the engine's ancestor of every slot (int32) when it resampled, else None."""
+    N = int(np.asarray(xe).size)
+    c = _StepCheck(N=N, seed=int(seed), rep=int(rep), epoch=int(epoch), thresh=float(thresh), bm24=int(bool(bm24)),
+                   regularize=int(bool(regularize)), u=float(u), z=float(np.asarray(z).reshape(-1)[0]),
+                   neff_e=float(neff_e), mean_e=float(mean_e), var_e=float(var_e), flag_e=int(bool(flag_e)))
+    x0 = np.ascontiguousarray(np.asarray(x0, float).reshape(-1))
+    w0 = np.ascontiguousarray(np.asarray(w0, float).reshape(-1))
+    xe = np.ascontiguousarray(np.asarray(xe, np.float32).reshape(-1))
+    le = np.ascontiguousarray(np.asarray(le, np.float32).reshape(-1))
+    a = None if anc is None else np.ascontiguousarray(np.asarray(anc, np.int32).reshape(-1))
+    if x0.size != N or w0.size != N or le.size != N or (a is not None and a.size != N):
+        raise ValueError("check_step: arrays of different lengths")
+    if load().pfo_sir_scalar_check_step(C.byref(model), C.byref(c), _p(x0), _p(w0), _p(xe, C.c_float),
+                                        _p(le, C.c_float), _p(a, C.c_int32)) != 0:
+        raise MemoryError("check_step: allocation failed")
+    out = {k: getattr(c, k) for k, _ in _StepCheck._fields_ if not k.startswith("_")}
+    for k in ("flag_e", "flag_o", "near_threshold"):
+        out[k] = bool(out[k])
     return out

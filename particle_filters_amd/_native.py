@@ -133,6 +133,8 @@ SIGNATURES = {
     "pf_last_run_resident": (C.c_int32, [_vp]),
     "pf_set_timing": (C.c_int32, [_vp, C.c_int32]),
     "pf_last_run_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
+    "pf_set_trace": (C.c_int32, [_vp, C.c_int64]),
+    "pf_get_trace": (C.c_int32, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp]),
     # include/pf_ledh.h
     "pf_ledh_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(LedhOpts), C.POINTER(_vp)]),
     "pf_ledh_destroy": (None, [_vp]),

@@ -7,7 +7,7 @@ synchronisation inside T (``pf_run`` in include/pf_engine.h).  The per-step
 outputs are exactly what the reference's driver loops collect
 (tests/integration_tests/test_pf_vs_simulator_sv.py:78-81;
 notebooks/PF_VS_experiments.ipynb cell 7): posterior means (post-resample, like
-``PFState.mean``), covariances (nx <= 4), pre-resample Neff, resample flags and
+``PFState.mean``), covariances (any nx), pre-resample Neff, resample flags and
 the log normaliser.
 
 Replicate r of a batch draws its randomness with Philox counter word

@@ -234,7 +234,13 @@ struct pf_handle {
   int cov_tc = 0;       // ring slots (steps) of partials
   int64_t cov_s0 = 0;   // first step of the pending chunk
   int cov_pending = 0;  // steps in the ring
+  bool cov_ready = false;  // every buffer above allocated and the geometry checked (ensure_cov)
   CovParams covp{};
+  // verification trace of resident runs (pf_set_trace; tests): [tr_T][R][Npad] each
+  float* tr_x = nullptr;
+  float* tr_l = nullptr;
+  int32_t* tr_anc = nullptr;
+  int64_t tr_T = 0;
   // live kernel timing (pf_set_timing): events recorded on the handle's stream right
   // before the first and after the last filter kernel of each pf_run_device
   bool timing = false;
@@ -538,36 +544,53 @@ pf_status apply_pending(pf_handle* h, const double* uniforms, const double* jitt
 // 4 waves over ~2048 waves per launch (or one block per replicate and block pair for nx > 48).
 // ---------------------------------------------------------------------------
 pf_status ensure_cov(pf_handle* h) {
-  if (h->xr || h->anc) return PF_OK;
-  CovParams& c = h->covp;
+  if (h->cov_ready) return PF_OK;
+  // The compiled register-state kernels write post-resample ancestors / rows only in k_step_grp;
+  // a compiled nx > 4 shape on plain k_step would leave anc / xr unwritten.
+  if (!h->ops->grp && !h->ops->dyn)
+    return fail(PF_E_UNSUPPORTED, "device-loop covariance: the step kernel writes no post-resample rows");
+  CovParams c = h->covp;
   c.N = h->N;
   c.Npad = h->Npad;
   c.nx = h->nx;
   c.nb = (h->nx + 15) / 16;
   c.npairs = c.nb * (c.nb + 1) / 2;
+  if (c.nb > 3 && c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
   c.P = c.npairs * 256 + c.nb * 16 + 1;
   c.cpb = cov_chunks_per_block(h->N, h->R);
   if (const char* e = std::getenv("PF_COV_CPB")) c.cpb = std::max(1, std::min(COV_CPB_MAX, std::atoi(e)));  // experiments
   c.nblk = (int)((h->N + (int64_t)COV_BLK * c.cpb - 1) / ((int64_t)COV_BLK * c.cpb));
-  if (h->regularize) HIPCHK(hipMalloc(&h->xr, (size_t)h->R * h->nx * h->Npad * h->esz));
-  else HIPCHK(hipMalloc((void**)&h->anc, (size_t)h->R * h->N * sizeof(int32_t)));
-  const size_t slot = (size_t)h->R * c.nblk * c.P * sizeof(double);
-  h->cov_tc = (int)std::max<size_t>(1, std::min<size_t>(32, ((size_t)256 << 20) / slot));  // <= 256 MiB of ring
-  HIPCHK(hipMalloc((void**)&h->cov_part, (size_t)h->cov_tc * slot));
-  HIPCHK(hipMalloc((void**)&h->cov_tot, (size_t)h->cov_tc * h->R * c.P * sizeof(double)));
-  h->cov_pending = 0;
   c.diag = std::getenv("PF_COV_DIAG") ? std::atoi(std::getenv("PF_COV_DIAG")) : 0;
-  if (c.nb > 3 && c.npairs > 65535) return fail(PF_E_UNSUPPORTED, "device-loop covariance: nx too large");
-  static bool attr_done = false;  // dynamic LDS above 64 KiB (fp64 rows, nb = 3)
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)cov_part_lds<double, 3>());
-    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)cov_part_lds<double, 2>());
-    (void)hipFuncSetAttribute((const void*)k_cov_part<double, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)cov_part_lds<double, 0>());
-    attr_done = true;
+  const size_t slot = (size_t)h->R * c.nblk * c.P * sizeof(double);
+  const int tc = (int)std::max<size_t>(1, std::min<size_t>(32, ((size_t)256 << 20) / slot));  // <= 256 MiB of ring
+  // allocate into locals; the handle takes them only when every allocation succeeded
+  void* xr = nullptr;
+  int32_t* anc = nullptr;
+  void* part = nullptr;
+  double* tot = nullptr;
+  hipError_t e = h->regularize ? hipMalloc(&xr, (size_t)h->R * h->nx * h->Npad * h->esz)
+                               : hipMalloc((void**)&anc, (size_t)h->R * h->N * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&part, (size_t)tc * slot);
+  if (e == hipSuccess) e = hipMalloc((void**)&tot, (size_t)tc * h->R * c.P * sizeof(double));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    for (void* q : {xr, (void*)anc, part, (void*)tot})
+      if (q) (void)hipFree(q);
+    return fail(PF_E_HIP, std::string("device-loop covariance buffers: ") + hipGetErrorString(e));
   }
+  // dynamic LDS above 64 KiB (fp64 rows, nb = 3): a per-device attribute, set on this handle's device
+  for (auto [fn, lds] : {std::pair<const void*, size_t>{(const void*)k_cov_part<double, 3>, cov_part_lds<double, 3>()},
+                         {(const void*)k_cov_part<double, 2>, cov_part_lds<double, 2>()},
+                         {(const void*)k_cov_part<double, 0>, cov_part_lds<double, 0>()}})
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  h->covp = c;
+  h->xr = xr;
+  h->anc = anc;
+  h->cov_part = part;
+  h->cov_tot = tot;
+  h->cov_tc = tc;
+  h->cov_pending = 0;
+  h->cov_ready = true;
   return PF_OK;
 }
 
@@ -738,6 +761,10 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   const char* hdr_env = std::getenv("PF_RES_HDR");  // PF_RES_HDR=0: always the records' prologue (tests)
   q.hdr_in = (hdr_env && std::atoi(hdr_env) == 0) ? 0ull : h->res_hdr;
   q.hdr_out = ++h->res_run;
+  q.tr_x = h->tr_x;
+  q.tr_l = h->tr_l;
+  q.tr_anc = h->tr_anc;
+  q.tr_T = h->tr_T;
   // Replicates are independent filters: when all R do not fit co-resident, groups of as many
   // as fit run one after another (each replicate computes exactly what it computes alone, so
   // the path - and every replicate's result - does not depend on R or on the sharding).
@@ -1079,7 +1106,8 @@ void pf_destroy(pf_handle* h) {
   for (double* q : h->lcum)
     if (q) (void)hipFree(q);
   for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
-                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->anc, (void*)h->cov_part, (void*)h->cov_tot})
+                  (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->anc, (void*)h->cov_part, (void*)h->cov_tot,
+                  (void*)h->tr_x, (void*)h->tr_l, (void*)h->tr_anc})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1373,6 +1401,56 @@ pf_status pf_set_timing(pf_handle* h, int32_t on) {
     HIPCHK(hipEventCreate(&h->tev[1]));
   }
   h->timing = on != 0;
+  return PF_OK;
+}
+
+pf_status pf_set_trace(pf_handle* h, int64_t T_cap) {
+  if (!h || T_cap < 0) return fail(PF_E_ARG, "bad argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (void* q : {(void*)h->tr_x, (void*)h->tr_l, (void*)h->tr_anc})
+    if (q) HIPCHK(hipFree(q));
+  h->tr_x = h->tr_l = nullptr;
+  h->tr_anc = nullptr;
+  h->tr_T = 0;
+  if (T_cap == 0) return PF_OK;
+  const size_t n = (size_t)T_cap * h->R * h->Npad;
+  float *x = nullptr, *l = nullptr;
+  int32_t* a = nullptr;
+  hipError_t e = hipMalloc((void**)&x, n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&l, n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&a, n * 4);
+  if (e == hipSuccess) e = hipMemsetAsync(a, 0xff, n * 4, h->stream);  // -1: slot not written
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    for (void* q : {(void*)x, (void*)l, (void*)a})
+      if (q) (void)hipFree(q);
+    return fail(PF_E_HIP, std::string("trace buffers: ") + hipGetErrorString(e));
+  }
+  h->tr_x = x;
+  h->tr_l = l;
+  h->tr_anc = a;
+  h->tr_T = T_cap;
+  return PF_OK;
+}
+
+pf_status pf_get_trace(pf_handle* h, int64_t t, int32_t r, float* x, float* l, int32_t* anc) {
+  if (!h || t < 0 || r < 0 || r >= h->R) return fail(PF_E_ARG, "bad argument");
+  if (t >= h->tr_T) return fail(PF_E_ARG, "step outside the trace (pf_set_trace)");
+  HIPCHK(hipSetDevice(h->device));
+  {
+    const pf_status s0 = settle(h);
+    if (s0) return s0;
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const size_t o = ((size_t)t * h->R + r) * h->Npad, n = (size_t)h->N * 4;
+  if (x) HIPCHK(hipMemcpy(x, h->tr_x + o, n, hipMemcpyDeviceToHost));
+  if (l) HIPCHK(hipMemcpy(l, h->tr_l + o, n, hipMemcpyDeviceToHost));
+  if (anc) {
+    HIPCHK(hipMemcpy(anc, h->tr_anc + o, n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemsetAsync(h->tr_anc + o, 0xff, n, h->stream));  // ready for the next run
+  }
   return PF_OK;
 }
 

@@ -774,6 +774,12 @@ struct EkfSpec {
 // The T loop (pf_ledh_run / pf_ledh_run_ekf): tracker covariances from the host (Ps) or from the
 // device EKF, all flow tables built up front, then flow -> weights -> resample -> moments per step.
 // EDH handles also take the tracker's past means Xb [T][nx] (host) or get them from the device EKF.
+// test hook: PF_TEST_LEDH_FAIL=1 reports the fused grid barrier as timed out after a completed run
+bool test_barrier_fail() {
+  const char* e = std::getenv("PF_TEST_LEDH_FAIL");
+  return e && std::atoi(e) == 1;
+}
+
 pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const EkfSpec* ekf, const double* Z,
                    const double* U, int64_t T, int32_t noise, double* means, double* covs, double* ess,
                    uint8_t* flags) {
@@ -831,6 +837,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     }
   }
   pf_status st = PF_OK;
+  bool touched = false;
   do {
     if ((Ps && hipMemcpyAsync(dP, S.data(), S.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
         hipMemcpyAsync(dZ, Z, (size_t)T * nz * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
@@ -921,6 +928,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       fp.ppb = h->fused_ppb;
     };
     size_t next_chunk = 0;
+    touched = true;  // from here on a failure leaves the particle state part-advanced
     for (int64_t t = 0; t < T && st == PF_OK; ++t) {
       if (ekf && next_chunk < cbeg.size() && t == cbeg[next_chunk] &&
           hipStreamWaitEvent(h->stream, evs[1 + next_chunk++], 0) != hipSuccess) {
@@ -996,7 +1004,7 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     }
     if (h->ferr) {
       unsigned int fe = 0;
-      if (hipMemcpy(&fe, h->ferr, 4, hipMemcpyDeviceToHost) != hipSuccess || fe != 0u) {
+      if (hipMemcpy(&fe, h->ferr, 4, hipMemcpyDeviceToHost) != hipSuccess || fe != 0u || test_barrier_fail()) {
         (void)hipMemset(h->ferr, 0, 8);
         st = lfail(PF_E_HIP, "run: fused step grid barrier timed out (workgroups not co-resident)");
         break;
@@ -1018,6 +1026,9 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
   cleanup();
   h->pending = false;
   h->rp_T = 0;  // a replay source serves one run
+  // A failed launch or a timed-out grid barrier leaves x / anc / w / the moment shifts part-advanced:
+  // the handle then reports 'not initialized' instead of continuing from a corrupt state.
+  if (st != PF_OK && touched) h->initialized = false;
   return st;
 }
 

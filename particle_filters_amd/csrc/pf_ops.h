@@ -166,26 +166,30 @@ struct ResidentLaunch {
   // launch).  Otherwise a plain launch after the same check against the occupancy API; the
   // kernel verifies co-residency itself either way (res_arrive / res_try_abort).
   // hipErrorCooperativeLaunchTooLarge -> the caller runs the launch-per-step path.
+  // p.tr_x set: the trace instance (the same kernel plus the verification-trace stores; tests)
   static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s, bool coop) {
-    const void* fn = (const void*)k_resident<float, NX, NZ, TK, OK>;
+    const bool tr = p.tr_x != nullptr;
+    const void* fn = tr ? (const void*)k_resident<float, NX, NZ, TK, OK, true> : (const void*)k_resident<float, NX, NZ, TK, OK>;
     if (coop) {
       ResParams q = p;
       void* args[] = {&q};
       return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
     }
-    if ((long long)G * R > (long long)cap()) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
+    if ((long long)G * R > (long long)(tr ? cap_of<true>() : cap())) return hipErrorCooperativeLaunchTooLarge;
+    if (tr) hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK, true>), dim3(G, R), dim3(RBS), 0, s, p);
+    else hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
     return hipGetLastError();
   }
   // CUs x workgroups per CU from the occupancy API, cached per device
-  static int cap() {
+  template <bool TR>
+  static int cap_of() {
     static int cached_dev = -1, cached_cap = 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (dev != cached_dev) {
       int cus = 0, per_cu = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_resident<float, NX, NZ, TK, OK>, RBS,
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_resident<float, NX, NZ, TK, OK, TR>, RBS,
                                                        0) != hipSuccess)
         return 0;
       cached_dev = dev;
@@ -193,6 +197,7 @@ struct ResidentLaunch {
     }
     return cached_cap;
   }
+  static int cap() { return cap_of<false>(); }
 };
 
 template <int NX, int NZ, int TK, int OK>

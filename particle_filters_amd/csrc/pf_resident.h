@@ -188,6 +188,15 @@ struct ResParams {
   // stored id skips the records' prologue (the host invalidates it on any other state write).
   unsigned long long* hdr;
   unsigned long long hdr_in, hdr_out;
+  // Verification trace (k_resident<..., TR = true> only; tests): for every VERIFIED step tv < tr_T
+  // of the launch - the version that was kept, after any rollback and recomputation - its
+  // predicted particles and pre-resample log-weights (any frame: the snapshot the verification
+  // read) into tr_x / tr_l [tr_T][Rtot][Npad], and on a resample step the ancestor of every
+  // output slot into tr_anc [tr_T][Rtot][Npad].
+  float* tr_x;
+  float* tr_l;
+  int32_t* tr_anc;
+  int64_t tr_T;
 };
 
 
@@ -351,7 +360,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
                                        double* Pl, double* Ck, double* offs, float* stage, int G, int b, int64_t N,
                                        unsigned nres,
                                        float m_g, double s0_g, double Mx, uint64_t seed, uint32_t rep,
-                                       uint32_t ep_res, int regularize, const Real* P) {
+                                       uint32_t ep_res, int regularize, const Real* P, int32_t* tanc) {
   using Mo = Model<Real, NX, NZ, TK, OK>;
   const int t = threadIdx.x;
   const int N32 = (int)N;  // resident grids: N <= RMAXG * RTILE < 2^31
@@ -445,6 +454,11 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
     is_src = c0 < o0 + RTILE && c1 > o0 && c1 > c0;
   }
   PF_GMARK(7);
+  if (tanc) {  // trace build: the ancestor of every offspring slot (tanc is a null constant otherwise)
+#pragma unroll
+    for (int e = 0; e < RPPT; ++e)
+      for (int i = cb[e]; i < cb[e + 1]; ++i) tanc[i] = i0 + e;
+  }
   for (int cs = R0; cs < R1; cs += RSTAGE) {
     const int ce = min(cs + RSTAGE, R1);
 #pragma unroll
@@ -529,7 +543,7 @@ __device__ __forceinline__ bool rb_gather(float* xn, unsigned long long* sflag, 
   return true;
 }
 
-template <typename Real, int NX, int NZ, int TK, int OK>
+template <typename Real, int NX, int NZ, int TK, int OK, bool TR = false>
 __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   static_assert(NX == 1 && sizeof(Real) == 4, "resident path: scalar fp32 state");
   using Mo = Model<Real, NX, NZ, TK, OK>;
@@ -1103,6 +1117,22 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     const bool dec = W * W < p.thresh * (double)N * W2;  // Neff = W^2 / W2 < thresh * N
 #endif
     const double Tv = lse_rel + Fv;
+    if constexpr (TR) {  // trace build: the verified step's predicted state, from its snapshot
+      if (tv < p.tr_T) {
+        const size_t to = ((size_t)tv * R + r) * (size_t)p.Npad;
+#pragma unroll
+        for (int q = 0; q < RPV; ++q) {
+          const float4 xs = snx[idx][q * RBS + t], ls = snl[idx][q * RBS + t];
+          const float xa[4] = {xs.x, xs.y, xs.z, xs.w}, la[4] = {ls.x, ls.y, ls.z, ls.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (i0 + 4 * q + e < p.Npad) {
+              p.tr_x[to + i0 + 4 * q + e] = xa[e];
+              p.tr_l[to + i0 + 4 * q + e] = la[e];
+            }
+        }
+      }
+    }
     if (b == G - 1 && t == 0) {  // outputs: the last workgroup (the partial tile, least work)
       const int64_t o = tv * R + r;
       p.o_neff[o] = (W * W) / W2;
@@ -1136,7 +1166,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     const uint32_t ep_res = p.ep0 + (uint32_t)(2 * tv + 1) - fo;
     if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.sflag + (size_t)r * RMAXG, p.flag0,
                                           p.err, &err_sh, snx[idx], snl[idx], red, Pl, Ck, offs, stage, G, b, N, nres, m_g,
-                                          s0_g, Mx, p.seed, rep, ep_res, p.regularize, (const Real*)p.P)) {
+                                          s0_g, Mx, p.seed, rep, ep_res, p.regularize, (const Real*)p.P,
+                                          (TR && tv < p.tr_T) ? p.tr_anc + ((size_t)tv * R + r) * (size_t)p.Npad
+                                                              : (int32_t*)nullptr)) {
       alive = false;
       break;
     }

@@ -145,8 +145,10 @@ class EDHFlowPF(LEDHFlowPF):
         (predict / get_past_mean / update, the same call sequence as the loop — it never sees
         the particles) unless ``tracker_seq = (Ps [T][nx][nx], Xbars [T][nx])`` is given.
         ``tracker="device"``: an EKFTracker over this filter's models runs on the GPU and
-        also yields the past means.  Process noise is Philox times chol(Q) (``"device"``) or
-        zero (``"none"``); resampling uniforms come from Philox."""
+        also yields the past means.  Process noise is Philox times chol(Q) (``"device"``,
+        resampling uniforms from Philox), zero (``"none"``) or replayed (``"host"`` with
+        ``replay=(V, U)``, the contract of ``LEDHFlowPF.run``: U[t] is read only on steps that
+        resample)."""
         if tracker not in ("host", "device"):
             raise ValueError("tracker must be 'host' or 'device'")
         if tracker == "device":

@@ -304,8 +304,12 @@ class LEDHFlowPF:
         unless ``tracker_covs`` [T][nx][nx] is given.  ``tracker="device"``: an EKFTracker over
         this filter's models runs on the GPU (analytic Jacobians), and its object is advanced
         to the final posterior afterwards.  Process noise is Philox times chol(Q)
-        (``"device"``) or zero (``"none"``, the reference default); resampling uniforms come
-        from Philox."""
+        (``"device"``, resampling uniforms from Philox), zero (``"none"``, the reference
+        default) or replayed (``"host"`` with ``replay=(V, U)``: V [T][N][nx] the
+        process_noise_sampler draws of each step, U [T] the systematic-resampling uniforms).
+        Replay contract: U[t] is read only on steps that resample, so lay it out with the
+        decisions you expect and check the returned flags against them.  A failed launch or
+        grid-barrier timeout leaves the filter uninitialised (AssertionError on the next call)."""
         if tracker not in ("host", "device"):
             raise ValueError("tracker must be 'host' or 'device'")
         self._adopt(state)

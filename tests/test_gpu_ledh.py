@@ -247,3 +247,30 @@ def test_fused_step_equals_kernel_chain(algo, monkeypatch):
     np.testing.assert_allclose(r1.covs, r0.covs, rtol=0, atol=1e-8 * max(1.0, float(np.abs(r0.covs).max())))
     np.testing.assert_allclose(x1, x0, rtol=0, atol=1e-9 * scale)
     np.testing.assert_allclose(w1, w0, rtol=1e-9, atol=1e-15)
+
+
+def test_fused_run_failure_poisons_handle(monkeypatch):
+    """A fused run whose grid barrier reports a timeout (hook PF_TEST_LEDH_FAIL=1) leaves its state
+    part-advanced: the handle must then refuse to continue (AssertionError 'Filter not initialized.'
+    from the next call) instead of filtering on from a corrupt state."""
+    om, gm, hm, g = case("l96")
+    ekf = TR.ExtendedKalmanFilter(gm, hm, om.Q, om.R, jac_g=gm.jacobian, jac_h=hm.jacobian)
+    tracker = TR.EKFTracker(ekf, TR.EKFState(np.asarray(g["mean0"], float).copy(),
+                                             np.asarray(g["cov0"], float).copy(), 0))
+    cfg = LD.LEDHConfig(n_particles=4096, n_lambda_steps=4, resample_ess_ratio=0.5, rng=np.random.default_rng(3))
+    pf = LD.LEDHFlowPF(tracker, gm, hm, hm.jacobian, M.GaussianTransitionDensity(gm, om.Q),
+                       M.GaussianLikelihood(hm, om.R), om.R, cfg, rng_mode="device")
+    st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+    Z = np.asarray(g["Z"], float)
+    pf.run(st, Z[:3], tracker="device")  # a good run first
+    monkeypatch.setenv("PF_TEST_LEDH_FAIL", "1")
+    with pytest.raises(Exception) as e:
+        pf.run(pf.state, Z[3:6], tracker="device")
+    assert "timed out" in str(e.value)
+    monkeypatch.delenv("PF_TEST_LEDH_FAIL")
+    with pytest.raises(AssertionError, match="Filter not initialized"):
+        pf.run(pf.state, Z[6:8], tracker="device")
+    # a fresh initialize makes the handle usable again
+    st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+    res = pf.run(st, Z[:3], tracker="device")
+    assert np.all(np.isfinite(res.means))

@@ -103,3 +103,73 @@ def test_exact_sv_likelihood_formula(golden_sv):
     np.testing.assert_allclose(c["w"], w, rtol=1e-9)
     np.testing.assert_allclose(c["means"][0], np.sum(w * x1), rtol=1e-10)
     np.testing.assert_allclose(c["neff"][0], 1.0 / np.sum(w ** 2), rtol=1e-9)
+
+
+def _engine_like_step(x0, w0, z, N, epoch, thresh=0.5, reg=False):
+    """The NumPy oracle's step (pinned to the reference) recorded the way the resident kernel's
+    trace records it: fp32 predicted particles and log-weights, int32 ancestors."""
+    from tests.teacher_forced import StepOracle
+    from oracle.pf_oracle import OracleState
+
+    ssm = ssm_oracle.sv_logsq(0.95, 0.2, 1.0)
+    o = StepOracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, seed=42, rep=0, bm24=True, epoch=epoch, Np=N,
+                   resample_thresh=thresh, resample_method="systematic", regularize_after_resample=reg,
+                   vectorized=True)
+    o.state = OracleState(x0[:, None].copy(), w0.copy(), np.zeros(1), np.eye(1), 0)
+    st = o.step(np.array([z]))
+    anc = None if o.idx is None else o.idx.astype(np.int32)
+    rec = dict(xe=o.pre_x[:, 0].astype(np.float32), le=np.log(o.pre_w).astype(np.float32), anc=anc,
+               neff_e=o.last_neff, flag_e=o.last_resampled, mean_e=float(st.mean[0]), var_e=float(st.cov[0, 0]))
+    return o, st, rec
+
+
+@pytest.mark.parametrize("reg", [False, True])
+def test_check_step_against_numpy_oracle(golden_sv, reg):
+    """oracle/sir_philox.c pfo_sir_scalar_check_step (the trace checker of the resident kernel's
+    in-launch steps, tests/test_gpu_resident_trace.py) reproduces the NumPy oracle's step: fed the
+    oracle's own step as the 'engine' record it measures fp32 rounding only, ancestors equal, and
+    its fp64 reference quantities (Neff, decision, moments) equal the NumPy oracle's."""
+    X, Y = golden_sv["X0"], golden_sv["Y0"]
+    N = 20000
+    rs = np.random.default_rng(5)
+    x0 = X[0] + 0.7 * rs.standard_normal(N)
+    w0 = rs.random(N) ** 8
+    w0 /= w0.sum()  # Neff well below N / 2: the step resamples
+    z = float(np.log(Y[3] ** 2))
+    o, st, rec = _engine_like_step(x0, w0, z, N, epoch=6, reg=reg)
+    assert o.last_resampled
+    c = SP.check_step(SP.sv_logsq_model(0.95, 0.2, 1.0), seed=42, rep=0, epoch=6, thresh=0.5, x0=x0, w0=w0, z=z,
+                      regularize=reg, **rec)
+    assert c["dx_pre"] <= 1e-6 and c["tv_w"] <= 1e-5 and c["dcdf"] <= 1e-5
+    np.testing.assert_allclose(c["neff_o"], o.last_neff, rtol=1e-12)
+    assert c["flag_o"] and c["n_anc_bad"] == 0 and c["n_anc_oracle_diff"] == 0
+    assert c["n_anc_self_diff"] <= 3 and c["max_margin_self"] <= 1e-6  # the fp32-rounded weights' own CDF
+    np.testing.assert_allclose(c["mean_o"], st.mean[0], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(c["var_o"], st.cov[0, 0], rtol=1e-9)
+    assert c["dmean"] <= 1e-13 and c["eps_w"] < 1e-4
+    # tampering: an ancestor moved to the next index, a non-monotone slot
+    bad = rec["anc"].copy()
+    bad[N // 2] += 1
+    c2 = SP.check_step(SP.sv_logsq_model(0.95, 0.2, 1.0), seed=42, rep=0, epoch=6, thresh=0.5, x0=x0, w0=w0, z=z,
+                       regularize=reg, **dict(rec, anc=bad))
+    assert c2["n_anc_oracle_diff"] >= 1 and c2["max_margin_oracle"] > 0.0
+    bad[N // 2 + 1] = 0
+    c3 = SP.check_step(SP.sv_logsq_model(0.95, 0.2, 1.0), seed=42, rep=0, epoch=6, thresh=0.5, x0=x0, w0=w0, z=z,
+                       regularize=reg, **dict(rec, anc=bad))
+    assert c3["n_anc_bad"] >= 1
+
+
+def test_check_step_no_resample(golden_sv):
+    X, Y = golden_sv["X0"], golden_sv["Y0"]
+    N = 8192
+    x0 = X[0] + 0.3 * np.random.default_rng(1).standard_normal(N)
+    w0 = np.full(N, 1.0 / N)
+    z = float(np.log(Y[2] ** 2))
+    o, st, rec = _engine_like_step(x0, w0, z, N, epoch=4, thresh=0.01)
+    assert not o.last_resampled
+    c = SP.check_step(SP.sv_logsq_model(0.95, 0.2, 1.0), seed=42, rep=0, epoch=4, thresh=0.01, x0=x0, w0=w0, z=z,
+                      **rec)
+    assert not c["flag_o"] and c["n_anc_oracle_diff"] == 0
+    np.testing.assert_allclose(c["mean_o"], st.mean[0], rtol=1e-12)
+    np.testing.assert_allclose(c["var_o"], st.cov[0, 0], rtol=1e-10)
+    assert c["dmean"] <= 1e-13
