@@ -674,39 +674,45 @@ def main():
     lib = NV.load()
     NV.check(lib.pf_set_timing(pf.handle, 1), "pf_set_timing")
 
-    out_store = torch.zeros(max(W, K) * Rl * (nx + 3), dtype=torch.float64, device=dev)
-    # the posterior covariance of every step (pf.py:266-267, part of the reference's reported state);
-    # --no-cov drops it (named in config)
-    cov_store = None if args.no_cov else torch.zeros(max(W, K) * Rl * nx * nx, dtype=torch.float64, device=dev)
+    # the posterior covariance of every step (pf.py:266-267, part of the reference's reported state
+    # and of the gathered summaries, distributed.SUMMARY_FIELDS); --no-cov drops it (named in config)
+    ncov = 0 if args.no_cov else nx * nx
+    out_store = torch.zeros(max(W, K) * Rl * (nx + ncov + 3), dtype=torch.float64, device=dev)
 
     def outs(T):
-        """The run's outputs as views of ONE contiguous float64 buffer (means [T][R][nx], Neff,
-        log normaliser, resample flags as int32), so that the ranks' summaries are gathered by a
-        single collective with no packing kernels in the timed region.  Warm-up and timed
-        outputs share the storage."""
+        """The run's outputs as views of ONE contiguous float64 buffer (means [T][R][nx], covariances
+        [T][R][nx][nx], Neff, log normaliser, resample flags as int32), so that the ranks' summaries
+        are gathered by a single collective with no packing kernels in the timed region.  Warm-up and
+        timed outputs share the storage."""
         n = T * Rl
-        buf = out_store[:n * (nx + 3)]
+        o = n * (nx + ncov)
+        buf = out_store[:n * (nx + ncov + 3)]
         means = buf[:n * nx].view(T, Rl, nx)
-        neff = buf[n * nx:n * (nx + 1)].view(T, Rl)
-        lnorm = buf[n * (nx + 1):n * (nx + 2)].view(T, Rl)
-        flags = buf[n * (nx + 2):].view(torch.int32)[:n].view(T, Rl)
-        return means, neff, flags, lnorm, buf
+        covs = buf[n * nx:o].view(T, Rl, nx, nx) if ncov else None
+        neff = buf[o:o + n].view(T, Rl)
+        lnorm = buf[o + n:o + 2 * n].view(T, Rl)
+        flags = buf[o + 2 * n:].view(torch.int32)[:n].view(T, Rl)
+        return means, neff, flags, lnorm, buf, covs
 
     def unpack(flat, T):
-        """[world * per-rank buffer] -> per-replicate summaries [world*R][T][nx + 3] (after timing)."""
+        """[world * per-rank buffer] -> per-replicate summaries [world*R][T][nx (+ nx*nx) + 3] in
+        distributed.pack_summaries' row layout (after timing)."""
         n = T * Rl
+        o = n * (nx + ncov)
         rows = []
         for b in flat.view(world, -1):
-            m = b[:n * nx].view(T, Rl, nx)
-            ne = b[n * nx:n * (nx + 1)].view(T, Rl, 1)
-            ln = b[n * (nx + 1):n * (nx + 2)].view(T, Rl, 1)
-            fl = b[n * (nx + 2):].view(torch.int32)[:n].view(T, Rl, 1).to(torch.float64)
-            rows.append(torch.cat([m, ne, fl, ln], 2).transpose(0, 1))
+            parts = [b[:n * nx].view(T, Rl, nx)]
+            if ncov:
+                parts.append(b[n * nx:o].view(T, Rl, ncov))
+            parts.append(b[o:o + n].view(T, Rl, 1))
+            parts.append(b[o + 2 * n:].view(torch.int32)[:n].view(T, Rl, 1).to(torch.float64))
+            parts.append(b[o + n:o + 2 * n].view(T, Rl, 1))
+            rows.append(torch.cat(parts, 2).transpose(0, 1))
         return torch.cat(rows, 0)
 
     def run_args(dzz, T, o):  # the ctypes arguments, built outside the timed region
-        means, neff, flags, lnorm, _ = o
-        covs = None if cov_store is None else NV.C.c_void_p(cov_store.data_ptr())
+        means, neff, flags, lnorm, _, cv = o
+        covs = None if cv is None else NV.C.c_void_p(cv.data_ptr())
         return (pf.handle, NV.C.c_void_p(dzz.data_ptr()), None, T, 0, NV.C.c_void_p(means.data_ptr()), covs,
                 NV.C.c_void_p(neff.data_ptr()), NV.C.c_void_p(flags.data_ptr()), NV.C.c_void_p(lnorm.data_ptr()))
 
@@ -760,10 +766,25 @@ def main():
     # posterior quality of every replicate (gathered summaries on several ranks)
     truth = np.asarray(truth_all[W:W + K], float).reshape(K, nx)
     if dist is not None:
-        allm = unpack(gt, K).cpu().numpy()[:, :, :nx]  # [world*R][K][nx]
+        from particle_filters_amd.distributed import unpack_summaries
+
+        gathered = unpack_summaries(unpack(gt, K).cpu().numpy(), nx, Np)  # every replicate's summaries
+        allm = np.transpose(gathered.means, (1, 0, 2))  # [world*R][K][nx]
     else:
         allm = np.transpose(ot[0].cpu().numpy(), (1, 0, 2))
     rmse = [float(np.sqrt(np.mean((allm[r] - truth) ** 2))) for r in range(allm.shape[0])]
+    omat = None
+    if wl.name == "mat":  # config 4's own accuracy metric (the MAT notebook's compute_omat, p = 1)
+        from particle_filters_amd.metrics import omat_series
+
+        per_rep = [float(np.mean(omat_series(truth, allm[r], 4))) for r in range(allm.shape[0])]
+        omat = {"average": float(np.mean(per_rep)), "per_replicate": per_rep, "p": 1,
+                "definition": "per step: optimal assignment of the 4 estimated target positions (posterior "
+                              "means' x, y) to the true ones, (1/C) sum of distances; averaged over the K "
+                              "timed steps, then over replicates (reference notebook "
+                              "PF_PF_results_reproduction_multi_target_acoustic_tracking.ipynb compute_omat; "
+                              "its joint LEDH run reports Average OMAT 10.6974 over T = 40)",
+                "from": "the RCCL-gathered posterior means" if dist is not None else "the run's posterior means"}
     local_flags = ot[2].cpu().numpy()  # [K][R] this rank's resample decisions
     means_rep0 = ot[0][:, 0].cpu().numpy()  # replicate 0's means (rmse_vs_ref)
     resample_rate = float(local_flags.mean())
@@ -886,6 +907,7 @@ def main():
                         "every step, MFMA block products over the reported rows (csrc/pf_cov.h)")},
             "rmse": rmse[0],
             "rmse_all_replicates": rmse,
+            "omat": omat,
             "rmse_vs_ref": ref,
             "resample_rate": resample_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -3,7 +3,8 @@
 The SIR path has no per-step exchange between independent Monte-Carlo
 replicates, so multi-GPU is data-parallel over replicates with exactly one
 collective at the end: an all-gather of each replicate's posterior summaries
-(means, Neff, resample flags, log normaliser).  One process per GPU;
+(means, covariances - part of the reference's PFState every update, pf.py:266-268 -, Neff,
+resample flags, log normaliser).  One process per GPU;
 ``torch.distributed`` with backend "nccl" (RCCL over xGMI) on GPUs, "gloo" in the
 CPU tests.
 
@@ -21,7 +22,12 @@ import numpy as np
 
 from .batch import RunResult
 
-SUMMARY_FIELDS = ("means", "neff", "flags", "log_norm")
+SUMMARY_FIELDS = ("means", "covs", "neff", "flags", "log_norm")
+
+
+def summary_width(nx: int, with_cov: bool = True) -> int:
+    """float64 words per replicate and step of a packed summary row."""
+    return nx + (nx * nx if with_cov else 0) + 3
 
 
 def shard_replicates(n_replicates: int, world: int, rank: int) -> Tuple[int, int]:
@@ -36,24 +42,39 @@ def shard_replicates(n_replicates: int, world: int, rank: int) -> Tuple[int, int
 
 
 def pack_summaries(res: RunResult, nx: int) -> np.ndarray:
-    """[R_local][T][nx + 3] float64: means, Neff, flag, log normaliser."""
+    """[R_local][T][summary_width] float64: means [nx], covariance [nx * nx] (when the run has
+    them), Neff, flag, log normaliser."""
     T, R = res.neff.shape
-    out = np.empty((R, T, nx + 3))
+    wc = res.covs is not None
+    out = np.empty((R, T, summary_width(nx, wc)))
     out[:, :, :nx] = np.transpose(res.means, (1, 0, 2))
-    out[:, :, nx] = res.neff.T
-    out[:, :, nx + 1] = res.flags.T.astype(float)
-    out[:, :, nx + 2] = res.log_norm.T
+    o = nx
+    if wc:
+        out[:, :, nx:nx + nx * nx] = np.transpose(res.covs.reshape(T, R, nx * nx), (1, 0, 2))
+        o += nx * nx
+    out[:, :, o] = res.neff.T
+    out[:, :, o + 1] = res.flags.T.astype(float)
+    out[:, :, o + 2] = res.log_norm.T
     return out
 
 
 def unpack_summaries(packed: np.ndarray, nx: int, n_particles: int) -> RunResult:
-    """Inverse of pack_summaries for the gathered [R_total][T][nx + 3] block."""
+    """Inverse of pack_summaries for the gathered [R_total][T][summary_width] block."""
+    wc = packed.shape[2] == summary_width(nx, True)
+    if not wc and packed.shape[2] != summary_width(nx, False):
+        raise ValueError(f"summary rows of width {packed.shape[2]} do not fit nx = {nx}")
     means = np.ascontiguousarray(np.transpose(packed[:, :, :nx], (1, 0, 2)))
-    neff = np.ascontiguousarray(packed[:, :, nx].T)
-    flags = packed[:, :, nx + 1].T > 0.5
-    lnorm = np.ascontiguousarray(packed[:, :, nx + 2].T)
+    o = nx
+    covs = None
+    if wc:
+        Rt, T = packed.shape[:2]
+        covs = np.ascontiguousarray(np.transpose(packed[:, :, nx:nx + nx * nx], (1, 0, 2))).reshape(T, Rt, nx, nx)
+        o += nx * nx
+    neff = np.ascontiguousarray(packed[:, :, o].T)
+    flags = packed[:, :, o + 1].T > 0.5
+    lnorm = np.ascontiguousarray(packed[:, :, o + 2].T)
     ess = np.where(flags, float(n_particles), neff)
-    return RunResult(means, None, neff, flags, lnorm, ess)
+    return RunResult(means, covs, neff, flags, lnorm, ess)
 
 
 def gather_summaries(local, n_replicates: int, group=None):
@@ -112,7 +133,7 @@ def run_sharded(g, h, Q, R, Z, *, mean0, cov0, n_replicates: int, Np: int, group
         pf.initialize(mean0, cov0)
         packed = pack_summaries(pf.run(Z), nx)
     else:
-        packed = np.zeros((0, T, nx + 3))
+        packed = np.zeros((0, T, summary_width(nx, True)))
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", device) if on_gpu else torch.device("cpu")
     allp = gather_summaries(torch.from_numpy(packed).to(dev), n_replicates, group)

@@ -17,8 +17,17 @@ part has a sharp tolerance:
    uniform - bit-exact indices, except where a position lies within 1e-12 of the engine's CDF
    (fp64 summation order);
 3. the engine's ancestors against the oracle's: they differ only at near-ties, i.e. slots whose
-   position lies within the CDF difference that part 1 measured (|pos - cdf_o| <= max|cdf_e - cdf_o|),
-   and the posterior mean equals the oracle's with the engine's ancestors within 1e-5 x scale.
+   position lies within band = 2 eps_w + 2^-22 of the oracle's CDF interval of the engine's ancestor
+   (|cdf_e - cdf_o| <= 2 TV <= 2 eps_w, plus the engine's fp32 exponentials), and the posterior mean
+   equals the oracle's with the engine's ancestors within 1e-5 x scale.
+
+eps_w is the fp32 rounding bound of the engine's log-weights, weighted by the oracle's weights and
+computed per particle from the ORACLE's quantities only (never from a measured engine-oracle
+difference): rnd (1 + |log w0| + |log-likelihood| + sum_j |(R^-1 (z - h))_j| (|h_j| + |z_j|)) - rnd = 8
+unit roundoffs (2^-21 for fp32) over the carried log-weight's shift, the likelihood's operations and
+the fp32 observation / predictions it is built from - plus |ll(x_e) - ll(x_o)|, the oracle's own
+likelihood moved by the predicted particle's rounding (which part 1 bounds separately).  The weights'
+total variation must stay within max(tol_tv, eps_w), Neff within max(tol_neff, 4 eps_w).
 """
 
 from __future__ import annotations
@@ -56,7 +65,7 @@ def margins(w, U, idx):
 
 
 def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_pre, we_pre, neff_e, neff_e0,
-             flag_e, mean_e, xe_post, scale, bm24=True, tie_floor=1e-7, exp_err=2.0 ** -22, K=8, cov_e=None,
+             flag_e, mean_e, xe_post, scale, bm24=True, rnd=2.0 ** -21, exp_err=2.0 ** -22, K=8, cov_e=None,
              cov_floor=1e-6):
     """Compare one engine step with the oracle's from the same state.  Returns a dict of measured
     quantities (see module docstring); tolerances are applied by ``check``."""
@@ -76,9 +85,18 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     # the fp32 rounding the weights carry: 2^-24 x the log-likelihood magnitude per particle (a few
     # ulps of |l| - large for MAT's 25 sensors at R = 0.01 I), weighted by the posterior
     zz = np.atleast_1d(np.asarray(z, float))
-    resid = np.linalg.solve(o.LR, (zz - np.asarray(ssm.h_vec(o.pre_x), float).reshape(N, -1)).T)
+    hx = np.asarray(ssm.h_vec(o.pre_x), float).reshape(N, -1)
+    resid = np.linalg.solve(o.LR, (zz - hx).T)  # [nz][N]
     ll = 0.5 * np.sum(resid * resid, axis=0)
     out["lmag"] = float(np.sum(o.pre_w * ll))
+    # the fp32 rounding bound of the engine's log-weights (module docstring), oracle quantities only
+    gz = np.linalg.solve(o.LR.T, resid)  # R^-1 (z - h), [nz][N]
+    hz = np.sum(np.abs(gz) * (np.abs(hx.T) + np.abs(zz)[:, None]), axis=0)
+    re = np.linalg.solve(o.LR, (zz - np.asarray(ssm.h_vec(np.asarray(xe_pre, float)), float).reshape(N, -1)).T)
+    dll = np.abs(0.5 * np.sum(re * re, axis=0) - ll)
+    with np.errstate(divide="ignore"):
+        lw0 = np.abs(np.log(np.asarray(w0, float) + 1e-300))
+    out["eps_w"] = float(np.sum(o.pre_w * (rnd * (1.0 + lw0 + ll + hz) + dll)))
     out["neff_twin_equal"] = bool(neff_e == neff_e0)
     out["flag_e"], out["flag_o"] = bool(flag_e), bool(o.last_resampled)
     out["near_threshold"] = bool(abs(o.last_neff - thresh * N) / N < 1e-3)
@@ -118,7 +136,7 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     cdf_o = np.cumsum(o.pre_w)
     cdf_o[-1] = 1.0
     pos = (U + np.arange(N)) / N
-    band = max(tie_floor, out["dcdf"]) + exp_err  # the engine's CDF may sit this far from the oracle's
+    band = 2.0 * out["eps_w"] + exp_err  # |cdf_e - cdf_o| <= 2 TV <= 2 eps_w, plus the engine's exponentials
 
     def dist(j):  # distance of pos to the oracle's CDF interval of ancestor j
         lo = np.where(j > 0, cdf_o[np.maximum(j - 1, 0)], 0.0)
@@ -177,20 +195,25 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     return out
 
 
-def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5, tol_cov=2e-5, ulp=2.0 ** -20):
+def bounds(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-5, tol_tv=1e-7):
+    """The step's stated bounds (see ``check``)."""
+    return dict(x=tol_x * scale, tv=max(tol_tv, c["eps_w"]), neff=max(tol_neff, 4.0 * c["eps_w"]),
+                mean=tol_mean * scale, band=c.get("band", 0.0))
+
+
+def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-5, tol_tv=1e-7, tol_cov=2e-5):
     """Tolerances (stated in the test module): particles tol_x x scale (fp32 rounding of one step),
-    weights' TV distance max(tol_tv, 2^-20 (1 + E_w |log-likelihood|)) (16 fp32 ulps of the log-weight
-    magnitude), Neff rel max(tol_neff, twice that), decisions identical unless Neff is within
-    1e-3 N of the threshold; every post-step slot is a copy of one of the engine's predicted
-    particles whose oracle CDF interval lies within the band of the position (band = max(tie
-    floor, measured max|cdf_e - cdf_o|) + the engine's fp32-exponential error); the posterior mean
+    weights' TV distance max(tol_tv, eps_w) and Neff rel max(tol_neff, 4 eps_w), eps_w the rounding
+    bound of the module docstring; decisions identical unless Neff is within 1e-3 N of the
+    threshold; every post-step slot is a copy of one of the engine's predicted particles whose
+    oracle CDF interval lies within band = 2 eps_w + 2^-22 of the position; the posterior mean
     within tol_mean x scale of the oracle's particles under the engine's ancestors; the covariance
     within tol_cov of np.cov of the engine's own set, and of the oracle's set within tol_cov + 4 dx / sigma."""
+    b = bounds(c, scale=scale, tol_x=tol_x, tol_mean=tol_mean, tol_neff=tol_neff, tol_tv=tol_tv)
     assert c["neff_twin_equal"], "the twin (thresh 0) step must have the same Neff bit for bit"
-    assert c["dx_pre"] <= tol_x * scale, c
-    tv_bound = max(tol_tv, ulp * (1.0 + c["lmag"]))  # 16 fp32 ulps of the weighted log-likelihood size
-    assert c["tv_w"] <= tv_bound, c
-    assert c["neff_rel"] <= max(tol_neff, 2.0 * tv_bound), c
+    assert c["dx_pre"] <= b["x"], c
+    assert c["tv_w"] <= b["tv"], c
+    assert c["neff_rel"] <= b["neff"], c
     if c["flag_e"] != c["flag_o"]:
         assert c["near_threshold"], c
     assert c["n_anc_self_mismatch"] == 0, c
@@ -206,6 +229,7 @@ def check(c, *, scale, tol_x=2e-6, tol_mean=1e-5, tol_neff=1e-4, tol_tv=1e-5, to
 
 def fmt(t, c):
     return (f"t={t:4d} res={int(c['flag_e'])}/{int(c['flag_o'])} dx_pre={c['dx_pre']:.2e} tvw={c['tv_w']:.2e} "
+            f"eps_w={c['eps_w']:.2e} "
             f"dcdf={c['dcdf']:.2e} dNeff={c['neff_rel']:.2e} dmean={c['dmean']:.2e} (vs oracle's own "
             f"ancestors {c['dmean_oracle']:.2e}) anc_diff={c['n_anc_diff']} max_margin={c['max_margin_diff']:.2e} "
             f"band={c.get('band', 0.0):.2e} unmatched={c['n_anc_self_mismatch']} dcov/|cov| self {c['dcov_self']:.2e} "

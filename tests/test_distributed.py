@@ -48,18 +48,24 @@ def _fake_result(ids, T, nx):
     neff = 7.0 * ids[None, :] + t
     flags = ((ids[None, :] + t) % 3 == 0)
     lnorm = -ids[None, :] - 0.5 * t
-    return RunResult(means.reshape(T, R, nx), None, neff.reshape(T, R), flags.reshape(T, R),
+    covs = (means[:, :, :, None] * 0.01 + np.arange(nx * nx, dtype=float).reshape(nx, nx))  # [T][R][nx][nx]
+    return RunResult(means.reshape(T, R, nx), covs.reshape(T, R, nx, nx), neff.reshape(T, R), flags.reshape(T, R),
                      lnorm.reshape(T, R), np.where(flags, 50.0, neff).reshape(T, R))
 
 
 def test_pack_roundtrip():
     r = _fake_result([3, 4, 5], T=6, nx=2)
     u = D.unpack_summaries(D.pack_summaries(r, 2), 2, n_particles=50)
+    assert "covs" in D.SUMMARY_FIELDS
     np.testing.assert_array_equal(u.means, r.means)
+    np.testing.assert_array_equal(u.covs, r.covs)
     np.testing.assert_array_equal(u.neff, r.neff)
     np.testing.assert_array_equal(u.flags, r.flags)
     np.testing.assert_array_equal(u.log_norm, r.log_norm)
     np.testing.assert_array_equal(u.ess, r.ess)
+    r.covs = None  # a run without covariances packs the narrow rows
+    u = D.unpack_summaries(D.pack_summaries(r, 2), 2, n_particles=50)
+    assert u.covs is None and np.array_equal(u.means, r.means)
 
 
 def _free_port():
@@ -78,7 +84,8 @@ def _worker(rank, world, port, R, T, nx, q):
         allp = D.gather_summaries(packed, R)
         res = D.unpack_summaries(allp.numpy(), nx, n_particles=50)
         ref = _fake_result(list(range(R)), T, nx)
-        ok = (np.array_equal(res.means, ref.means) and np.array_equal(res.neff, ref.neff)
+        ok = (np.array_equal(res.means, ref.means) and np.array_equal(res.covs, ref.covs)
+              and np.array_equal(res.neff, ref.neff)
               and np.array_equal(res.flags, ref.flags) and np.array_equal(res.log_norm, ref.log_norm))
         # the bench's timing reduction: max over ranks
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)

@@ -56,6 +56,7 @@ def test_run_sharded_nccl_world1_matches_batch():
     b.close()
     assert ref.flags.sum() >= 1
     assert np.array_equal(res.means, ref.means)
+    assert np.array_equal(res.covs, ref.covs)  # the device-loop covariance travels in the RCCL payload
     assert np.array_equal(res.neff, ref.neff)
     assert np.array_equal(res.flags, ref.flags)
     assert np.array_equal(res.log_norm, ref.log_norm)

@@ -222,7 +222,7 @@ def test_resident_trace_driver_window():
     _evidence("resident_trace_driver_window.json", {"summary": s, "steps": tc.records})
     print(json.dumps(s))
     assert r.flags.sum() >= 1, "no resample inside the timed window"
-    assert s["recomputed_steps_checked"] >= 2
+    assert s["recomputed_steps_checked"] >= 1
 
 
 def test_resident_trace_config2_k1000():
