@@ -374,6 +374,8 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
         data_desc = "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)"
         notes = ("N=1e4 particles, 8 lambda steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
                  "(analytic RK4 Jacobian), Philox process noise")
+    ltraffic = pmc_traffic("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
+                           "k_flow_wave" if per_particle else "k_ledh_fused")[0]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -421,8 +423,9 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
                                      "note": "EKF stepped on the host in NumPy, covariances uploaded, same device loop"},
             "roofline": {"bound": "fp64-valu", "achieved": flops / dev_s / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / dev_s / 1e12 / FP64_VALU_PEAK_TFLOPS,
-                         "traffic": pmc_traffic("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
-                                                "k_flow_wave" if per_particle else "k_ledh_fused")[0],
+                         "traffic": ltraffic,
+                         "traffic_gbs": None if ltraffic is None else ltraffic / (dev_s / K) / 1e9,
+                         "traffic_frac": None if ltraffic is None else ltraffic / (dev_s / K) / 1e9 / HBM_PEAK_GBS,
                          "traffic_unit": "HBM bytes per filter step of the kernel (rocprofv3 FETCH_SIZE x2 + "
                                          "WRITE_SIZE, profiles/pmc_traffic_<workload>.json)",
                          "kernel": ("whole LEDH job: k_ekf_seq + " + ("per step k_flow_wave (per-particle flow)"
@@ -912,6 +915,9 @@ def main():
             "resample_rate": resample_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         # the HBM fraction on the bytes the counters saw move (FETCH x2 + WRITE per step)
+                         "traffic_gbs": None if traffic is None else traffic / step_s / 1e9,
+                         "traffic_frac": None if traffic is None else traffic / step_s / 1e9 / HBM_PEAK_GBS,
                          "kernel": f"pf::{kname}<{real},{ktmpl}>",
                          "steps_per_launch": K if resident else 1,
                          "algorithmic_bytes_per_step": alg_bytes_run / K,

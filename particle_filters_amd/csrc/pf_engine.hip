@@ -320,7 +320,8 @@ bool choose_geometry(pf_handle* h) {
 size_t step_lds(const pf_handle* h, bool gather) {
   if (h->ops->dyn)  // tile CDF / per-particle weights (doubles) + ancestor slots (ints)
     return base_lds_bytes(h->G) + (size_t)h->tile * (sizeof(double) + sizeof(int));
-  const size_t epi = (size_t)h->ops->rec_size * sizeof(double);
+  size_t epi = (size_t)h->ops->rec_size * sizeof(double);
+  if (h->nx == 1 && h->ops->prec == PF_PRECISION_FP32) epi = std::max(epi, (size_t)MERGE_LDS_BYTES);
   size_t gat = gather ? (size_t)h->tile * (sizeof(double) + sizeof(int)) : 0;
   if (gather && h->sys_cdf) gat += (size_t)SYS_STAGE * h->tile * sizeof(double) + 16;  // staged source tiles
   return base_lds_bytes(h->G) + std::max(epi, gat);

@@ -732,6 +732,42 @@ struct WAcc {
     }
     out[0] = M;
   }
+  // The same merge with one wave instead of all: every thread stages (m, s...) in LDS (stage:
+  // [NS + 1][BS] floats), then wave 0 alone rescales and sums them - lane l takes threads l, l + 64,
+  // ... (fp32 rescale factors, fp64 sums), then one DPP sum per field.  The other waves do no
+  // reduction arithmetic at all (fp32 scalar-state step: ~1/8 of its VALU was the merge).
+  template <int BS>
+  __device__ __forceinline__ void block_merge_lds(float* stage, double* out) {
+    static_assert(sizeof(Real) == 4, "fp32 engine");
+    constexpr int K = BS / 64;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    stage[t] = m;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) stage[(1 + i) * BS + t] = s[i];
+    __syncthreads();
+    if (w != 0) return;
+    float mk[K];
+    float Ml = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      mk[k] = stage[k * 64 + lane];
+      Ml = fmaxf(Ml, mk[k]);
+    }
+    double acc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float f = (mk[k] > -INFINITY) ? __expf(mk[k] - Ml) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) acc[i] = fma((double)stage[(1 + i) * BS + k * 64 + lane], (double)(i == 1 ? f * f : f), acc[i]);
+    }
+    const float Mw = wave_max_u(Ml);
+    const double g = (Ml > -INFINITY) ? (double)__expf(Ml - Mw) : 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) out[1 + i] = wave_sum_ud(acc[i] * (i == 1 ? g * g : g));
+    out[0] = Mw;
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -757,7 +793,11 @@ struct StepTraits {
 };
 
 // LDS carve (doubles): [0, LDS_RED) scratch | Pl[G+1] | tile area (cdf doubles + anc ints, or
-// the staged epilogue record)
+// the staged epilogue record, and for the fp32 scalar state the record merge's staging after it)
+#ifndef PF_MERGE_LDS
+#define PF_MERGE_LDS 0
+#endif
+constexpr int MERGE_LDS_BYTES = 32 * 8 + 5 * 256 * 4;  // record slots + [NS + 1][BS] floats (NX = 1, BS = 256)
 constexpr int LDS_RED = 512;
 constexpr int LDS_PL = LDS_RED;
 __host__ __device__ constexpr int lds_tile(int G) { return LDS_PL + ((G + 8) & ~7); }
@@ -1111,7 +1151,14 @@ k_step(StepParams p) {
   __syncthreads();    // all tile-CDF / ancestor reads are done
   if (p.do_update) {
     double w[1 + WA::NS];
-    acc.template block_merge<BS>(red, w);
+#if PF_MERGE_LDS
+    if constexpr (NX == 1 && sizeof(Real) == 4) {  // staged after the record's slots (step_lds: MERGE_LDS_BYTES)
+      static_assert((WA::NS + 1) * BS * 4 + 32 * 8 <= MERGE_LDS_BYTES && RC::SIZE <= 32, "merge staging");
+      acc.template block_merge_lds<BS>((float*)(cdf + 32), w);
+    }
+    else
+#endif
+      acc.template block_merge<BS>(red, w);
     if (t == 0) {
       fin[RC::M] = w[0];
       fin[RC::S0] = w[1];

@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       const double wi = c0 == 0 ? w1 : p.f.w_in[i];
       double eta[PER];
       const double l =
-          flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, c0 == 0 ? x1 : nullptr, zs);
+          flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, x1, zs, c0 == 0);
 #ifdef PF_STAMPS
       asm volatile("" ::"v"(l));
       if (c0 == 0) LF_STAMP(11);

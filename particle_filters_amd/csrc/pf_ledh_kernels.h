@@ -563,14 +563,18 @@ template <int NX, int NZ, int TK>
 // when the previous step's resample is applied here, k_ledh_fused)
 // (xpre: the lane's PER components of that row, already loaded by the caller, or null)
 __device__ __forceinline__ void group_prior(const FlowParams& p, const double* __restrict__ Pm, int64_t i, int64_t src,
-                                            int q, int base, double* gx, double* v, const double* xpre = nullptr) {
+                                            int q, int base, double* gx, double* v, const double* xpre = nullptr,
+                                            bool use_pre = false) {
   using L = Lay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  // xpre (when given) always points at the caller's register array and use_pre picks its values:
+  // a pointer chosen at run time between that array and null would force the array into scratch
   double x[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int a = q * PER + j;
-    x[j] = xpre ? xpre[j] : (a < NX ? p.x_in[(int64_t)a * p.Npad + src] : 0.0);
+    const double xm = (a < NX && !(xpre && use_pre)) ? p.x_in[(int64_t)a * p.Npad + src] : 0.0;
+    x[j] = (xpre && use_pre) ? xpre[j] : xm;
   }
 #ifdef PF_STAMPS
   asm volatile("" ::"v"(x[0]));
@@ -712,12 +716,13 @@ template <int NX, int NZ, int TK>
 __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
                                                       const double* __restrict__ af, int64_t i, int64_t src, int q,
                                                       int base, double* eta, double w_i,
-                                                      const double* xpre = nullptr, const double* zz = nullptr) {
+                                                      const double* xpre = nullptr, const double* zz = nullptr,
+                                                      bool use_pre = false) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
   double gx[PER], v[PER];
-  group_prior<NX, NZ, TK>(p, Pm, i, src, q, base, gx, v, xpre);
+  group_prior<NX, NZ, TK>(p, Pm, i, src, q, base, gx, v, xpre, use_pre);
 #ifdef PF_STAMPS
   asm volatile("" ::"v"(v[PER - 1]), "v"(gx[PER - 1]));
   LF_STAMP(8);

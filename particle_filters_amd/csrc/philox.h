@@ -29,11 +29,16 @@ struct u32x4 {
   uint32_t x, y, z, w;
 };
 
+// PF_PHILOX_ROUNDS: experiment builds only (timing ablations, tools/build_sv_variants.sh); the
+// shipped library and the oracle use the 10 rounds of Philox4x32-10.
+#ifndef PF_PHILOX_ROUNDS
+#define PF_PHILOX_ROUNDS 10
+#endif
 __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < PF_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)M0 * c.x;
     const uint64_t p1 = (uint64_t)M1 * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../particle_filters_amd/csrc"
 B=../../build/csrc
 name=$1; unit=$2; flags=$3
 OTHERS=""
-for o in pf_diag pf_engine pf_inst_linear pf_inst_l96 pf_inst_mat pf_inst_sv pf_ledh; do
+for o in pf_diag pf_engine pf_inst_linear pf_inst_l96 pf_inst_mat pf_inst_sv pf_inst_dyn pf_ledh; do
   [ "$o" = "$unit" ] || OTHERS="$OTHERS $B/$o.o"
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-pass-failed $flags \

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-4 measurement call: VALU issue costs (tools/valu_probe.hip) and same-box A/B of
+# experiment libraries (build/libpf_hip_<name>.so, tools/build_sv_variants.sh / build_inst_variant.sh).
+#   tools/gpu_probe.sh OUTDIR
+D=${1:-gpurun_out/probe}
+mkdir -p "$D"; . "$(dirname "$0")/gpu_lib.sh"
+B=particle_filters_amd/libpf_hip.so
+step valu 120 build/valu_probe
+for rep in 1 2; do
+  for lib in $B build/libpf_hip_r6.so; do
+    PF_LIB=$lib step "k1000_$(basename $lib .so)_$rep" 120 python -u bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-ref
+  done
+  for lib in $B build/libpf_hip_r6.so build/libpf_hip_mlds.so; do
+    PF_LIB=$lib step "sv64_$(basename $lib .so)_$rep" 180 python -u bench.py --workload sv64 --steps 30 --warmup 5 --no-cpu-baseline --no-ref
+  done
+  for lib in $B build/libpf_hip_ledhold.so; do
+    PF_LIB=$lib step "ledh_$(basename $lib .so)_$rep" 180 python -u bench.py --workload ledh --steps 100 --warmup 10 --no-cpu-baseline --no-ref
+  done
+done
+echo done >> "$D/steps.log"
