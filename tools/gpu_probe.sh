@@ -6,9 +6,12 @@ D=${1:-gpurun_out/probe}
 mkdir -p "$D"; . "$(dirname "$0")/gpu_lib.sh"
 B=particle_filters_amd/libpf_hip.so
 step valu 120 build/valu_probe
+PF_LIB=build/libpf_hip_ldspub.so PF_EVIDENCE_DIR=$D/ev_ldspub step trace_ldspub 300 python -u -m pytest tests/test_gpu_resident_trace.py -x -q --timeout 250 --timeout-method thread
+PF_LIB=build/libpf_hip_mlds.so PF_EVIDENCE_DIR=$D/ev_mlds step tf_mlds 300 python -u -m pytest tests/test_gpu_teacher_forced.py::test_step_sv64 -x -q --timeout 250 --timeout-method thread
 for rep in 1 2; do
-  for lib in $B build/libpf_hip_r6.so; do
+  for lib in $B build/libpf_hip_r6.so build/libpf_hip_ldspub.so; do
     PF_LIB=$lib step "k1000_$(basename $lib .so)_$rep" 120 python -u bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-ref
+    PF_LIB=$lib step "k20_$(basename $lib .so)_$rep" 120 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref
   done
   for lib in $B build/libpf_hip_r6.so build/libpf_hip_mlds.so; do
     PF_LIB=$lib step "sv64_$(basename $lib .so)_$rep" 180 python -u bench.py --workload sv64 --steps 30 --warmup 5 --no-cpu-baseline --no-ref
