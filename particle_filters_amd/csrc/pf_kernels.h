@@ -849,6 +849,16 @@ k_step(StepParams p) {
   Real sx[SC][NX], sl[SC], sll[SC], sn[SC][NX];
   Real px[4], pl[4];  // scalar state: the thread's second chunk, loaded with the first
   bool pre1 = false;
+  // fp32 scalar state (the sv64 roofline run): the second chunk is speculated too (qx, qll), and a
+  // launch that does not gather finishes both chunks straight from registers (no per-particle
+  // branches, one max-first pass over the thread's 8 particles) instead of the generic chunk loop
+#ifndef PF_STEP_FAST
+#define PF_STEP_FAST 1
+#endif
+  constexpr bool FAST2 = PF_STEP_FAST && NX == 1 && CH == 4 && sizeof(Real) == 4;
+  constexpr int QC = FAST2 ? 4 : 1;
+  Real qx[QC], qll[QC];
+  bool spec1 = false;  // qx / qll hold the second chunk's predicted particles and log-likelihoods
   Real z[NZ];
   if (p.do_update) {
 #pragma unroll
@@ -898,6 +908,24 @@ k_step(StepParams p) {
             M::add_lower(sx[e], sn[e], P, M::L::LQ);
           }
           sll[e] = (p.do_update == 1) ? M::loglik(sx[e], z, P, p.r_diag != 0) : Real(0);
+        }
+      }
+      if constexpr (FAST2) {
+        if (pre1 && p.do_predict && p.do_update == 1) {
+          const int64_t i1 = o0 + (int64_t)(t + BS) * CH;
+          Real n4[4];
+          chunk_normals4<Real>(p.seed, i1, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4,
+                               p.pbase);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {  // slots past o1 are never stored nor weighed
+            Real xe[1] = {px[e]};
+            M::transition(xe, P, u);
+            Real ne[1] = {n4[e]};
+            M::add_lower(xe, ne, P, M::L::LQ);
+            qx[e] = xe[0];
+            qll[e] = M::loglik(xe, z, P, p.r_diag != 0);
+          }
+          spec1 = true;
         }
       }
     }
@@ -1008,7 +1036,64 @@ k_step(StepParams p) {
   const Real lse_r = (Real)lse_prev;
   const bool write_x = p.do_predict || p.allow_gather;  // gather launches always produce x_out
 
-  for (int c = t; c < nchunks; c += BS) {
+  // fast finish of the fp32 scalar step (uniform per workgroup): every chunk of the thread was
+  // speculated and nothing is gathered
+  bool fast = false;
+  if constexpr (FAST2) {
+#ifndef PF_NO_PRE1
+    constexpr int SPEC_CHUNKS = 2;
+#else
+    constexpr int SPEC_CHUNKS = 1;
+#endif
+    fast = !gather && p.do_predict && p.do_update == 1 && nchunks <= SPEC_CHUNKS * BS;
+    if (fast && t < nchunks) {
+      const Real lu = (Real)lprev_uniform;
+      const int64_t ia = o0 + (int64_t)t * CH, ib = o0 + (int64_t)(t + BS) * CH;
+      const int na = (int)min((int64_t)4, o1 - ia), nb = spec1 ? (int)min((int64_t)4, o1 - ib) : 0;
+      Real lp[8], xv[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xv[e] = e < na ? sx[e][0] : Real(0);  // slots past the tile: zero weight, finite value
+        lp[e] = e < na ? (h.uniform ? lu : sl[e] - lse_r) + sll[e] : -INFINITY;
+        xv[4 + e] = e < nb ? qx[e] : Real(0);
+        lp[4 + e] = e < nb ? (h.uniform ? lu : pl[e] - lse_r) + qll[e] : -INFINITY;
+      }
+      Real m = lp[0];
+#pragma unroll
+      for (int e = 1; e < 8; ++e) m = fmaxf(m, lp[e]);
+      acc.m = m;
+      if (m > -INFINITY) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const Real we = (lp[e] > -INFINITY) ? exp_r<Real>(lp[e] - m) : Real(0);
+          acc.s[0] += we;
+          acc.s[1] += we * we;
+          acc.s[2] += we * xv[e];
+          acc.s[3] += we * xv[e] * xv[e];
+        }
+      }
+      if (na == 4) {
+        store4<Real>(x_out + ia, xv);
+        store4<Real>(lw_out + ia, lp);
+      } else {
+        for (int e = 0; e < na; ++e) {
+          x_out[ia + e] = xv[e];
+          lw_out[ia + e] = lp[e];
+        }
+      }
+      if (nb == 4) {
+        store4<Real>(x_out + ib, xv + 4);
+        store4<Real>(lw_out + ib, lp + 4);
+      } else {
+        for (int e = 0; e < nb; ++e) {
+          x_out[ib + e] = xv[4 + e];
+          lw_out[ib + e] = lp[4 + e];
+        }
+      }
+    }
+  }
+
+  for (int c = t; c < (fast ? 0 : nchunks); c += BS) {
     const int64_t i0 = o0 + (int64_t)c * CH;
     const bool first = PRE && c == t;
     const bool spec = first && !gather;  // predicted x and loglik already computed

@@ -31,7 +31,8 @@ rounding through the likelihood's slopes (sir_philox.c) - a formula, not a measu
                           and ancestors
   posterior variance      <= (2e-5 + 4 dx / sigma) x max(var, (1e-6 scale)^2)
   chained state           after the launch, the engine's state is exactly the traced chain's
-                          (particles bitwise, weights rel 1e-6)
+                          (particles bitwise; weights rel 8 x 2^-24 (1 + max|l|): the exit log-weights
+                          are the last traced ones shifted by <= 3 verified frame deltas in fp32)
 Every measured quantity and its bound per step goes to $PF_EVIDENCE_DIR (default
 gpurun_out/evidence) as JSON; the round's copy is kept under profiles/.
 """
@@ -134,10 +135,13 @@ class TraceChain:
             else:
                 x = xe.astype(float)
                 w = we
-        # the chained state IS the engine's state after the launch
+        # the chained state IS the engine's state after the launch: particles bitwise; the exit
+        # log-weights are the last traced ones shifted by the frame deltas of the steps verified after
+        # it (at most LAG + 1 = 3), each rounded to fp32: rel <= 8 x 2^-24 (1 + max |l|)
         xf, wf = pf.particles()[0, :, 0], pf.weights()[0]
         assert np.array_equal(xf, x), f"{label}: exit particles differ from the traced chain"
-        np.testing.assert_allclose(wf, w, rtol=1e-6, atol=1e-12 / N)
+        lmax = 0.0 if flag else float(np.max(np.abs(le[np.isfinite(le)])))
+        np.testing.assert_allclose(wf, w, rtol=8.0 * 2.0 ** -24 * (1.0 + lmax), atol=1e-12 / N)
         NV.check(self.lib.pf_set_trace(pf.handle, 0), "pf_set_trace")
         return res
 
