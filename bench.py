@@ -492,6 +492,53 @@ def cpu_baseline_numpy(wl, Z, mean0, cov0):
                       f"(oracle/pf_oracle.py vectorized=True, BLAS limited to 1 thread), {dt:.1f} s"}
 
 
+def _numpy_replicate_worker(args):
+    """One core's share of cpu_baseline_numpy_cores: an independent replicate (its own seed) of the
+    vectorised restatement, BLAS on one thread; returns (particle-steps, seconds) of the timed steps."""
+    name, rep, steps, Z, mean0, cov0, start_at = args
+    from threadpoolctl import threadpool_limits
+
+    from oracle import pf_oracle
+
+    wl = WORKLOADS[name]()
+    if name == "mat":
+        wl.build(max(steps, 1), 0)  # the sensor grid the oracle's model needs
+    ssm = wl.oracle_ssm()
+    with threadpool_limits(limits=1):
+        pf = pf_oracle.SIROracle(ssm.g_vec, ssm.h_vec, ssm.Q, ssm.R, Np=wl.n_particles,
+                                 rng=np.random.default_rng(42 + rep), vectorized=True)
+        pf.initialize(np.asarray(mean0, float), np.asarray(cov0, float))
+        while time.time() < start_at:  # every worker starts its timed steps together
+            time.sleep(0.001)
+        t0 = time.perf_counter()
+        for t in range(steps):
+            pf.step(Z[t])
+        dt = time.perf_counter() - t0
+    return wl.n_particles * steps, dt
+
+
+def cpu_baseline_numpy_cores(wl, Z, mean0, cov0):
+    """BASELINE.md 3 for the replicate configurations: the vectorised NumPy restatement on every core
+    of this process's CPU share at once, one independent replicate per core (one process each, BLAS
+    on one thread), on a bounded sample; aggregate = sum of the workers' particle-steps/s."""
+    import multiprocessing as mp
+
+    cores = oracle_threads()
+    steps = min(int(os.environ.get("PF_CPU_CORES_STEPS", str(max(2, wl.cpu_steps)))), len(Z))
+    Zs = np.asarray(Z[:steps], float)
+    start_at = time.time() + 20.0 + 0.5 * cores  # after every worker has imported and initialised
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_numpy_replicate_worker, [(wl.name, r, steps, Zs, mean0, cov0, start_at) for r in range(cores)])
+    rates = [n / dt for n, dt in res]
+    return {"value": float(sum(rates)), "unit": "particle-steps/s", "cores": cores, "kind": "port",
+            "per_core": float(np.mean(rates)), "host_cores": os.cpu_count(),
+            "sample": f"{wl.name}: {cores} independent replicates of N={wl.n_particles:.0e}, one process per core "
+                      f"(spawned), {steps} steps each, vectorised NumPy restatement (oracle/pf_oracle.py "
+                      f"vectorized=True, BLAS 1 thread per process), timed steps started together; "
+                      f"slowest worker {max(dt for _, dt in res):.1f} s"}
+
+
 def oracle_threads():
     """Threads of the C/OpenMP leg: this process's CPU share.  On the GPU pool a one-GPU box is
     allotted 16 host CPUs (OMP_NUM_THREADS is set to it there); os.cpu_count() reports the whole
@@ -848,6 +895,14 @@ def main():
             except Exception as e:
                 errors.append(f"numpy restatement: {e!r}")
                 log("cpu numpy baseline failed:", repr(e))
+            if wl.replicates > 1 and wl.nx > 1:  # the replicate configuration on every core of the box
+                try:
+                    if cpu is None:
+                        cpu = {"value": None, "unit": "particle-steps/s", "cores": 1, "kind": "port"}
+                    cpu["numpy_vectorised_all_cores"] = cpu_baseline_numpy_cores(wl, Zall[W:], s0, cov0)
+                except Exception as e:
+                    errors.append(f"numpy restatement on all cores: {e!r}")
+                    log("cpu numpy all-cores baseline failed:", repr(e))
             if wl.name in ("sv", "sv64"):
                 try:
                     c1 = cpu_c1_full_run()
