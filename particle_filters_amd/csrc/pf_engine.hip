@@ -236,17 +236,6 @@ struct pf_handle {
   int cov_pending = 0;  // steps in the ring
   bool cov_ready = false;  // every buffer above allocated and the geometry checked (ensure_cov)
   CovParams covp{};
-  // overlapped covariance (cov_ovl): k_cov_part of step s - 1 runs on cov_stream while step s + 1
-  // runs; a third x / lw buffer and a second ancestor (or jittered-row) buffer keep its inputs
-  // until it is done (cov_done[s % 4] waited for by step s + 3, the next writer of those buffers)
-  bool cov_ovl = false;
-  hipStream_t cov_stream = nullptr;
-  void* x_spare = nullptr;
-  void* lw_spare = nullptr;
-  void* xr2 = nullptr;
-  int32_t* anc2 = nullptr;
-  hipEvent_t step_done[4] = {nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t cov_done[4] = {nullptr, nullptr, nullptr, nullptr};
   // verification trace of resident runs (pf_set_trace; tests): [tr_T][R][Npad] each
   float* tr_x = nullptr;
   float* tr_l = nullptr;
@@ -603,20 +592,6 @@ pf_status ensure_cov(pf_handle* h) {
   h->cov_tc = tc;
   h->cov_pending = 0;
   h->cov_ready = true;
-  // the overlap's buffers and stream (PF_COV_OVERLAP=0: the covariance runs in the step stream)
-  const char* ov = std::getenv("PF_COV_OVERLAP");
-  if (!(ov && ov[0] == '0')) {
-    const size_t xbytes = (size_t)h->R * h->nx * h->Npad * h->esz, lwbytes = (size_t)h->R * h->Npad * h->esz;
-    bool ok = hipMalloc(&h->x_spare, xbytes) == hipSuccess && hipMalloc(&h->lw_spare, lwbytes) == hipSuccess &&
-              (h->regularize ? hipMalloc(&h->xr2, xbytes) == hipSuccess
-                             : hipMalloc((void**)&h->anc2, (size_t)h->R * h->N * sizeof(int32_t)) == hipSuccess) &&
-              hipStreamCreateWithFlags(&h->cov_stream, hipStreamNonBlocking) == hipSuccess;
-    for (int k = 0; ok && k < 4; ++k)
-      ok = hipEventCreateWithFlags(&h->step_done[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&h->cov_done[k], hipEventDisableTiming) == hipSuccess;
-    if (!ok) (void)hipGetLastError();
-    h->cov_ovl = ok;  // else the serial path (its buffers stay allocated until destroy)
-  }
   return PF_OK;
 }
 
@@ -627,7 +602,7 @@ void launch_cov_part(dim3 grid, const CovParams& c, hipStream_t s) {
 }
 
 // The pending chunk of the ring -> d_covs[s0 .. s0 + pending)
-pf_status flush_cov(pf_handle* h, double* d_covs, hipStream_t st) {
+pf_status flush_cov(pf_handle* h, double* d_covs) {
   if (h->cov_pending == 0) return PF_OK;
   const CovParams& c = h->covp;
   CovFin f;
@@ -642,10 +617,10 @@ pf_status flush_cov(pf_handle* h, double* d_covs, hipStream_t st) {
   f.nb = c.nb;
   f.npairs = c.npairs;
   const unsigned nr = (unsigned)(h->cov_pending * h->R);
-  if (f.part_f32) hipLaunchKernelGGL(k_cov_fin_sum<float>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, st, f);
-  else hipLaunchKernelGGL(k_cov_fin_sum<double>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, st, f);
+  if (f.part_f32) hipLaunchKernelGGL(k_cov_fin_sum<float>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
+  else hipLaunchKernelGGL(k_cov_fin_sum<double>, dim3((unsigned)((c.P + 255) / 256), nr), dim3(256), 0, h->stream, f);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_cov_fin_out, dim3((unsigned)((h->nx * h->nx + 255) / 256), nr), dim3(256), 0, st, f);
+  hipLaunchKernelGGL(k_cov_fin_out, dim3((unsigned)((h->nx * h->nx + 255) / 256), nr), dim3(256), 0, h->stream, f);
   HIPCHK(hipGetLastError());
   h->cov_pending = 0;
   return PF_OK;
@@ -654,17 +629,16 @@ pf_status flush_cov(pf_handle* h, double* d_covs, hipStream_t st) {
 // Covariance of step s (its predicted rows xs / log-weights lw; the post-resample rows in h->xr,
 // written by the gather that followed) from the step's outputs (flag, lse, mean): its block
 // partials into the ring; d_covs[s] when the chunk is flushed (full, or the end of the run).
-pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, const void* xr, const int32_t* anc, int64_t s,
-                     const double* d_means, const int32_t* d_flags, const double* d_lse, double* d_covs,
-                     hipStream_t st) {
+pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, const double* d_means,
+                     const int32_t* d_flags, const double* d_lse, double* d_covs) {
   CovParams c = h->covp;
   const int R = h->R;
   if (h->cov_pending == 0) h->cov_s0 = s;
   if (s != h->cov_s0 + h->cov_pending) return fail(PF_E_ARG, "device-loop covariance: steps out of order");
   c.part = (double*)h->cov_part + (size_t)h->cov_pending * R * c.nblk * c.P;
   c.xs = xs;
-  c.xr = xr;
-  c.anc = anc;
+  c.xr = h->xr;
+  c.anc = h->anc;
   c.lw = lw;
   c.flag = d_flags + s * R;
   c.lse = d_lse + s * R;
@@ -673,21 +647,21 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, const void* x
   if (c.nb <= 3) {
     const dim3 grid((unsigned)c.nblk, (unsigned)R);
     if (f32) {
-      if (c.nb == 1) launch_cov_part<float, 1>(grid, c, st);
-      else if (c.nb == 2) launch_cov_part<float, 2>(grid, c, st);
-      else launch_cov_part<float, 3>(grid, c, st);
+      if (c.nb == 1) launch_cov_part<float, 1>(grid, c, h->stream);
+      else if (c.nb == 2) launch_cov_part<float, 2>(grid, c, h->stream);
+      else launch_cov_part<float, 3>(grid, c, h->stream);
     } else {
-      if (c.nb == 1) launch_cov_part<double, 1>(grid, c, st);
-      else if (c.nb == 2) launch_cov_part<double, 2>(grid, c, st);
-      else launch_cov_part<double, 3>(grid, c, st);
+      if (c.nb == 1) launch_cov_part<double, 1>(grid, c, h->stream);
+      else if (c.nb == 2) launch_cov_part<double, 2>(grid, c, h->stream);
+      else launch_cov_part<double, 3>(grid, c, h->stream);
     }
   } else {
     const dim3 grid((unsigned)c.nblk, (unsigned)R, (unsigned)c.npairs);
-    if (f32) launch_cov_part<float, 0>(grid, c, st);
-    else launch_cov_part<double, 0>(grid, c, st);
+    if (f32) launch_cov_part<float, 0>(grid, c, h->stream);
+    else launch_cov_part<double, 0>(grid, c, h->stream);
   }
   HIPCHK(hipGetLastError());
-  if (++h->cov_pending == h->cov_tc) return flush_cov(h, d_covs, st);
+  if (++h->cov_pending == h->cov_tc) return flush_cov(h, d_covs);
   return PF_OK;
 }
 
@@ -1134,13 +1108,8 @@ void pf_destroy(pf_handle* h) {
     if (q) (void)hipFree(q);
   for (void* p : {h->wbuf, (void*)h->cdf, h->P, h->d_z, h->d_u, (void*)h->d_out, (void*)h->d_replay_a,
                   (void*)h->d_replay_b, (void*)h->d_unif, h->xr, (void*)h->anc, (void*)h->cov_part, (void*)h->cov_tot,
-                  (void*)h->tr_x, (void*)h->tr_l, (void*)h->tr_anc, h->x_spare, h->lw_spare, h->xr2, (void*)h->anc2})
+                  (void*)h->tr_x, (void*)h->tr_l, (void*)h->tr_anc})
     if (p) (void)hipFree(p);
-  for (int k = 0; k < 4; ++k) {
-    if (h->step_done[k]) (void)hipEventDestroy(h->step_done[k]);
-    if (h->cov_done[k]) (void)hipEventDestroy(h->cov_done[k]);
-  }
-  if (h->cov_stream) (void)hipStreamDestroy(h->cov_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -1361,33 +1330,6 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     p.xr_out = h->xr;  // one of the two: rows with jitter, ancestors without
     p.anc_out = h->anc;
   }
-  // Overlapped covariance: step s writes its x / lw into the buffer that step s - 3 wrote (a third
-  // buffer rotates through x[cx ^ 1] / lw[clw ^ 1]) and its ancestors into buffer s % 2, so the
-  // covariance of step s - 1 (launched after step s on cov_stream) keeps its inputs until step s + 2
-  // - which waits for it - replaces them.
-  const bool ovl = cov_loop && h->cov_ovl;
-  int32_t* anc_b[2] = {h->anc, h->anc2};
-  void* xr_b[2] = {h->xr, h->xr2};
-  auto ovl_before_step = [&](int64_t s, bool writes_x, bool writes_lw) -> pf_status {
-    if (!ovl) return PF_OK;
-    if (s >= 3) HIPCHK(hipStreamWaitEvent(h->stream, h->cov_done[(s - 3) & 3], 0));
-    if (writes_x) std::swap(h->x[h->cx ^ 1], h->x_spare);
-    if (writes_lw) std::swap(h->lw[h->clw ^ 1], h->lw_spare);
-    p.anc_out = anc_b[s & 1];
-    p.xr_out = xr_b[s & 1];
-    return PF_OK;
-  };
-  // the covariance of step s - 1: its predicted rows / log-weights and the ancestors step s wrote
-  auto cov_after_step = [&](int64_t s, const void* xs, const void* lw) -> pf_status {
-    if (!ovl) return launch_cov(h, xs, lw, h->xr, h->anc, s - 1, d_means, d_flags, d_lse, d_covs, h->stream);
-    HIPCHK(hipEventRecord(h->step_done[s & 3], h->stream));
-    HIPCHK(hipStreamWaitEvent(h->cov_stream, h->step_done[s & 3], 0));
-    pf_status st = launch_cov(h, xs, lw, xr_b[s & 1], anc_b[s & 1], s - 1, d_means, d_flags, d_lse, d_covs,
-                              h->cov_stream);
-    if (st) return st;
-    HIPCHK(hipEventRecord(h->cov_done[(s - 1) & 3], h->cov_stream));
-    return PF_OK;
-  };
   p.o_neff = d_neff;
   p.o_lse = d_lse;
   p.o_flag = d_flags;
@@ -1411,12 +1353,10 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
       if (st) return st;
     }
     const void *xs_prev = h->x[h->cx], *lw_prev = h->lw[h->clw];  // step s - 1's predicted state
-    pf_status st = ovl_before_step(s, predict || gather_possible, true);
-    if (st) return st;
-    st = launch_step(h, p, predict || gather_possible, true, true);
+    pf_status st = launch_step(h, p, predict || gather_possible, true, true);
     if (st) return st;
     if (cov_loop && s >= 1) {
-      st = cov_after_step(s, xs_prev, lw_prev);
+      st = launch_cov(h, xs_prev, lw_prev, s - 1, d_means, d_flags, d_lse, d_covs);
       if (st) return st;
     }
     prev_res = h->epoch++;
@@ -1437,19 +1377,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     if (st) return st;
   }
   const void *xs_last = h->x[h->cx], *lw_last = h->lw[h->clw];
-  pf_status st = ovl_before_step(T, true, false);
-  if (st) return st;
-  st = launch_step(h, p, true, false, true);
+  pf_status st = launch_step(h, p, true, false, true);
   if (st) return st;
   if (cov_loop) {
-    st = cov_after_step(T, xs_last, lw_last);
+    st = launch_cov(h, xs_last, lw_last, T - 1, d_means, d_flags, d_lse, d_covs);
     if (st) return st;
-    st = flush_cov(h, d_covs, ovl ? h->cov_stream : h->stream);
+    st = flush_cov(h, d_covs);
     if (st) return st;
-    if (ovl) {  // the run ends when its covariances are done: the step stream waits for them
-      HIPCHK(hipEventRecord(h->cov_done[T & 3], h->cov_stream));
-      HIPCHK(hipStreamWaitEvent(h->stream, h->cov_done[T & 3], 0));
-    }
   }
   p.out_step = -1;
   p.out_post_step = T - 1;

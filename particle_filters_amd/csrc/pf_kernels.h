@@ -698,6 +698,24 @@ struct WAcc {
         for (int f = d; f < NX; ++f) s[c++] += e * x[d] * x[f];
     }
   }
+  // The thread's particles in one max-first pass (fp32 scalar state, 8 particles: chunk t, then
+  // chunk t + BS): no per-particle rescale.  Slots past the tile carry l = -inf, x = 0.
+  __device__ __forceinline__ void add_maxfirst8(const Real (&l)[8], const Real (&x)[8]) {
+    static_assert(NX == 1, "scalar state");
+    Real mm = l[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) mm = fmaxf(mm, l[e]);
+    m = mm;
+    if (!(mm > -INFINITY)) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const Real we = (l[e] > -INFINITY) ? exp_r<Real>(l[e] - mm) : Real(0);
+      s[0] += we;
+      s[1] += we * we;
+      s[2] += we * x[e];
+      s[3] += we * x[e] * x[e];
+    }
+  }
   // Block merge (max first): result (m, s...) in out[0..NS] of thread 0 only.
   // red >= (BS/64)*(NS+1) doubles.
   template <int BS>
@@ -735,7 +753,8 @@ struct WAcc {
   // The same merge with one wave instead of all: every thread stages (m, s...) in LDS (stage:
   // [NS + 1][BS] floats), then wave 0 alone rescales and sums them - lane l takes threads l, l + 64,
   // ... (fp32 rescale factors, fp64 sums), then one DPP sum per field.  The other waves do no
-  // reduction arithmetic at all (fp32 scalar-state step: ~1/8 of its VALU was the merge).
+  // reduction arithmetic at all.  The fp32 scalar step's default (PF_MERGE_LDS): sv64 306 -> 279
+  // us/step in a same-box A/B (profiles/r04/ab).
   template <int BS>
   __device__ __forceinline__ void block_merge_lds(float* stage, double* out) {
     static_assert(sizeof(Real) == 4, "fp32 engine");
@@ -795,7 +814,7 @@ struct StepTraits {
 // LDS carve (doubles): [0, LDS_RED) scratch | Pl[G+1] | tile area (cdf doubles + anc ints, or
 // the staged epilogue record, and for the fp32 scalar state the record merge's staging after it)
 #ifndef PF_MERGE_LDS
-#define PF_MERGE_LDS 0
+#define PF_MERGE_LDS 1
 #endif
 constexpr int MERGE_LDS_BYTES = 32 * 8 + 5 * 256 * 4;  // record slots + [NS + 1][BS] floats (NX = 1, BS = 256)
 constexpr int LDS_RED = 512;
@@ -850,8 +869,8 @@ k_step(StepParams p) {
   Real px[4], pl[4];  // scalar state: the thread's second chunk, loaded with the first
   bool pre1 = false;
   // fp32 scalar state (the sv64 roofline run): the second chunk is speculated too (qx, qll), and a
-  // launch that does not gather finishes both chunks straight from registers (no per-particle
-  // branches, one max-first pass over the thread's 8 particles) instead of the generic chunk loop
+  // launch that does not gather finishes both chunks straight from registers (straight-line code,
+  // no per-chunk reloads, bounds tests or pointer bookkeeping) instead of the generic chunk loop
 #ifndef PF_STEP_FAST
 #define PF_STEP_FAST 1
 #endif
@@ -1058,20 +1077,11 @@ k_step(StepParams p) {
         xv[4 + e] = e < nb ? qx[e] : Real(0);
         lp[4 + e] = e < nb ? (h.uniform ? lu : pl[e] - lse_r) + qll[e] : -INFINITY;
       }
-      Real m = lp[0];
-#pragma unroll
-      for (int e = 1; e < 8; ++e) m = fmaxf(m, lp[e]);
-      acc.m = m;
-      if (m > -INFINITY) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const Real we = (lp[e] > -INFINITY) ? exp_r<Real>(lp[e] - m) : Real(0);
-          acc.s[0] += we;
-          acc.s[1] += we * we;
-          acc.s[2] += we * xv[e];
-          acc.s[3] += we * xv[e] * xv[e];
-        }
-      }
+      // max-first over the thread's 8 particles - the same pass the generic loop makes for this
+      // geometry (klp / kx below), so a step computed here and the same step computed there (e.g.
+      // after an in-kernel gather) give bitwise the same records: a run cut into segments stays
+      // bitwise the uninterrupted run
+      acc.add_maxfirst8(lp, xv);
       if (na == 4) {
         store4<Real>(x_out + ia, xv);
         store4<Real>(lw_out + ia, lp);
@@ -1093,6 +1103,22 @@ k_step(StepParams p) {
     }
   }
 
+  // generic loop in the fast path's geometry (<= 2 chunks per thread, fp32 scalar): the particles are
+  // kept and accumulated max-first after the loop, exactly as the fast path does
+  bool fastgeo = false;
+  Real klp[QC * 2], kx[QC * 2];
+  if constexpr (FAST2) {
+#ifndef PF_NO_PRE1
+    fastgeo = nchunks <= 2 * BS;
+#else
+    fastgeo = nchunks <= BS;
+#endif
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      klp[e] = -INFINITY;
+      kx[e] = Real(0);
+    }
+  }
   for (int c = t; c < (fast ? 0 : nchunks); c += BS) {
     const int64_t i0 = o0 + (int64_t)c * CH;
     const bool first = PRE && c == t;
@@ -1201,7 +1227,21 @@ k_step(StepParams p) {
       }
       if (p.do_update) {
         lp[e] = lp[e] + ll[e];  // log(w_prev) - quad/2  (do_update == 2: reweigh only, ll = 0)
-        acc.add(lp[e], xe);
+        if constexpr (FAST2) {
+          if (fastgeo) {
+            if (c == t) {
+              klp[e] = lp[e];
+              kx[e] = xe[0];
+            } else {
+              klp[4 + e] = lp[e];
+              kx[4 + e] = xe[0];
+            }
+          } else {
+            acc.add(lp[e], xe);
+          }
+        } else {
+          acc.add(lp[e], xe);
+        }
       }
     }
     if constexpr (CH == 4) {
@@ -1226,6 +1266,9 @@ k_step(StepParams p) {
         for (int d = 0; d < NX; ++d) x_out[(int64_t)d * p.Npad + i0] = x[0][d];
       if (p.do_update) lw_out[i0] = lp[0];
     }
+  }
+  if constexpr (FAST2) {
+    if (fastgeo && !fast && p.do_update && t < nchunks) acc.add_maxfirst8(klp, kx);
   }
   PF_STAMP(4);
 

@@ -86,13 +86,6 @@ constexpr unsigned RSPIN_LIMIT = 1u << 24;
 #define PF_RSTAGE 8192
 #endif
 constexpr int RSTAGE = PF_RSTAGE;  // rollback scatter staging chunk (floats of LDS)
-// PF_RES_LDSPUB: the step record from LDS-staged thread partials reduced by the publishing wave
-// alone (no per-wave DPP reductions), double-buffered by iteration parity inside the rollback
-// staging area (which is used only inside a rollback, after the iteration's publish)
-#ifndef PF_RES_LDSPUB
-#define PF_RES_LDSPUB 0
-#endif
-static_assert(!PF_RES_LDSPUB || 2 * 5 * PF_RBS <= PF_RSTAGE, "staged partials fit the rollback staging area");
 
 // Diagnostic phase accounting (PF_STAMPS builds only): workgroup 0, thread 0
 // accumulates s_memrealtime ticks (100 MHz) per phase into g_pf_stamps[0..15].
@@ -834,23 +827,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 #ifdef PF_YOUNG_PRIO
       if (w >= RCW) __builtin_amdgcn_s_setprio(2);
 #endif
-#if PF_RES_LDSPUB
-      {  // this thread's partials for the publishing wave; aux sums (rare: just gathered) per wave
-        float* sp = stage + cur * (5 * RBS);
-        sp[t] = m;
-        sp[RBS + t] = s0;
-        sp[2 * RBS + t] = s00;
-        sp[3 * RBS + t] = s1;
-        sp[4 * RBS + t] = s2;
-        if (have_aux) {
-          const double a1 = wave_sum_ud(aux1), a2 = wave_sum_ud(aux2);
-          if (lane == 0) {
-            mslot[cur][w][5] = a1;
-            mslot[cur][w][6] = a2;
-          }
-        }
-      }
-#else
       // wave partials (DPP), one LDS slot per wave
       const float Mw = wave_max_u(m);
       const float fw = (m > -INFINITY) ? __expf(m - Mw) : 0.0f;
@@ -872,7 +848,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         mslot[cur][w][5] = a1;
         mslot[cur][w][6] = a2;
       }
-#endif
       {  // snapshot of this step in slot s_next % NSNAP
         const int slot = (int)(s_next % NSNAP);
 #pragma unroll
@@ -948,46 +923,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       // the older wave stalls, and the record is on every workgroup's critical path (-4%/step)
       if (w == PF_PUBW) __builtin_amdgcn_s_setprio(3);
 #endif
-#if PF_RES_LDSPUB
-      if (w == PF_PUBW) {
-        // lane l reduces threads l, l + 64, ...: one rescale per thread to the tile max (fp32
-        // factors), the tile mass in fp64, then one DPP sum per field
-        const float* sp = stage + cur * (5 * RBS);
-        float mk[RNW];
-        float Ml = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < RNW; ++k) {
-          mk[k] = sp[k * 64 + lane];
-          Ml = fmaxf(Ml, mk[k]);
-        }
-        const float Mt = wave_max_u(Ml);
-        double q0 = 0.0;
-        float q00 = 0.0f, q1 = 0.0f, q2 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < RNW; ++k) {
-          const float fk = (mk[k] > -INFINITY) ? __expf(mk[k] - Mt) : 0.0f;
-          q0 = fma((double)sp[RBS + k * 64 + lane], (double)fk, q0);
-          q00 = fmaf(sp[2 * RBS + k * 64 + lane], fk * fk, q00);
-          q1 = fmaf(sp[3 * RBS + k * 64 + lane], fk, q1);
-          q2 = fmaf(sp[4 * RBS + k * 64 + lane], fk, q2);
-        }
-        const double S0 = wave_sum_ud(q0);
-        const float S00 = wave_sum_u(q00), S1 = wave_sum_u(q1), S2 = wave_sum_u(q2);
-        if (lane < RF * RCOPIES) {
-          const int f = lane % RF, c = lane / RF;
-          double A = 0.0;
-          if (rec_aux && (f == 5 || f == 6))
-#pragma unroll
-            for (int j = 0; j < RNW; ++j) A += mslot[cur][j][f];
-          const unsigned long long sb = (unsigned long long)__double_as_longlong(S0);
-          const unsigned pay = f == 0 ? __float_as_uint(Mt) : f == 1 ? (unsigned)(sb >> 32) : f == 7 ? (unsigned)sb
-                             : f == 2 ? __float_as_uint(S00) : f == 3 ? __float_as_uint(S1) : f == 4 ? __float_as_uint(S2)
-                             : __float_as_uint((float)A);
-          unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
-          st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
-        }
-      }
-#else
       if (w == PF_PUBW && lane < RF * RCOPIES) {
         const int f = lane % RF, c = lane / RF;
         const int src = (f == 7) ? 1 : f;  // the S0 low word is the same fp64 sum as the high word
@@ -1023,7 +958,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         unsigned long long* g = p.gran + (size_t)c * cstride + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
         st_sc1(g + f * RMAXG, ((unsigned long long)(p.tag0 + s_next + 1) << 32) | pay);
       }
-#endif
 #if PF_PUB_PRIO && !defined(PF_PRIO_STICKY)
       if (w == PF_PUBW) __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1343,25 +1277,6 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     }
   }
 
-#if PF_RES_LDSPUB
-  if (alive && !last_uniform) {  // the exit records below read the last computed step's wave partials
-    const float* sp = stage + last_cur * (5 * RBS);
-    const float m = sp[t], s0 = sp[RBS + t], s00 = sp[2 * RBS + t], s1 = sp[3 * RBS + t], s2 = sp[4 * RBS + t];
-    const float Mw = wave_max_u(m);
-    const float fw = (m > -INFINITY) ? __expf(m - Mw) : 0.0f;
-    const double w0 = wave_sum_ud((double)s0 * (double)fw);
-    const float w00 = wave_sum_u(s00 * fw * fw);
-    const float w1 = wave_sum_u(s1 * fw), w2 = wave_sum_u(s2 * fw);
-    if (lane == 0) {
-      mslot[last_cur][w][0] = Mw;
-      mslot[last_cur][w][1] = w0;
-      mslot[last_cur][w][2] = w00;
-      mslot[last_cur][w][3] = w1;
-      mslot[last_cur][w][4] = w2;
-    }
-    __syncthreads();
-  }
-#endif
   // ---- exit state in the k_step layout ---------------------------------------
   if (i0 + RPPT <= N) {
 #pragma unroll
