@@ -34,6 +34,7 @@
 #include "pf_dpp.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "philox.h"
 #include "pf_models.h"
@@ -591,6 +592,157 @@ __device__ __forceinline__ int prefix_tile(const double* Pl, int G, double pos) 
   return lo < G ? lo : G - 1;
 }
 
+// Number of systematic positions below x: #{ i in [0, N) : (U + i) / N < x } (pf.py:146-171 compares
+// pos = (U + arange(N)) / N < cdf[j] in fp64).  Exactly, (U + i) / N < x <=> i < y = x N - U; the fp64
+// division can disagree only when y is within ~1e-10 of an integer, and only then are the candidate
+// positions evaluated the reference's way.  32-bit slot indices (k_step: N < 2^31).
+__device__ __forceinline__ int sys_count_exact(double x, double U, int N, int c) {
+  const double Nd = (double)N;
+  while (c > 0 && (U + (double)(c - 1)) / Nd >= x) --c;
+  while (c < N && (U + (double)c) / Nd < x) ++c;
+  return c;
+}
+__device__ __forceinline__ int sys_count_below(double x, double U, int N) {
+  const double y = fma(x, (double)N, -U);
+  const double fl = floor(y), d = y - fl;
+  const int c = (int)fmin(fmax(fl + 1.0, 0.0), (double)N);
+  if (d > 1e-7 && d < 1.0 - 1e-7) return c;
+  return sys_count_exact(x, U, N, c);
+}
+
+// block maximum of floats (every thread gets it); redf >= BS / 64 floats, free on entry
+template <int BS>
+__device__ __forceinline__ float block_max_f(float v, float* redf) {
+  constexpr int NW = BS / 64;
+  const float wm = wave_max_u(v);
+  if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = wm;
+  __syncthreads();
+  float M = redf[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) M = fmaxf(M, redf[i]);
+  return M;
+}
+
+// exclusive block max-scan of ints (-1 below thread 0); redi >= BS / 64 ints
+template <int BS>
+__device__ __forceinline__ int block_excl_max_i(int v, int* redi) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o);
+    if (lane >= o) incl = max(incl, u);
+  }
+  int ex = __shfl_up(incl, 1);
+  if (lane == 0) ex = -1;
+  __syncthreads();
+  if (lane == 63) redi[w] = incl;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NW; ++i)
+    if (i < w) ex = max(ex, redi[i]);
+  return ex;
+}
+
+// Systematic ancestors of slots [o0, o1) of a replicate (pf.py:146-171: the ancestor of slot i is the
+// first j with (U + i) / N < cdf[j], the last particle if none), source-driven and search-free.  The
+// source tiles k whose prefix ranges [Pl[k], Pl[k+1]) hold some of the slots (the tile of a position
+// as prefix_tile finds it) each build their fp64 CDF segment cdf[j] = Pl[k] + c_k sum_{j' <= j}
+// e^(l_j' - m_k), c_k = e^(m_k - M) / S (thread t: elements [t per, t per + per), a DPP block scan of
+// the thread sums), and particle j's offspring start at slot L_j = C(cdf[j - 1]) (cdf[-1] = Pl[k];
+// C = sys_count_below): the owner of slot i is the last particle with L_j <= i.  Each particle marks
+// its first slot in anc_l with an LDS max (particles starting before this workgroup's slots mark the
+// first slot, one max per thread), and an inclusive max-scan over the slots fills the runs (ancestor
+// indices increase with the slot).  The tile's slot range is [C(Pl[k]), C(Pl[k+1])): L_0 = C(Pl[k])
+// by construction, so consecutive tiles meet exactly.
+template <typename Real, int NX, int BS, int PM>
+__device__ __forceinline__ void sys_ancestors(const Real* __restrict__ lw_in, const double* rec_in, int G, int64_t N,
+                                              int tile, int64_t o0, int64_t o1, double U, const Head& h,
+                                              const double* Pl, int* anc_l, double* red, bool stamp_on) {
+  (void)stamp_on;
+  const int t = threadIdx.x;
+  const int N32 = (int)N, w0 = (int)o0, w1 = (int)o1, nsl = w1 - w0;
+  for (int s = t; s < nsl; s += BS) anc_l[s] = -1;  // ordered before the marks by the scans' barriers
+  const double Nd = (double)N;
+  const int klo = prefix_tile(Pl, G, (U + (double)w0) / Nd);
+  const int khi = prefix_tile(Pl, G, (U + (double)(w1 - 1)) / Nd);
+  PF_STAMP(6);
+  int ntiles = 0;
+  // log-weights of <= PM per thread in registers (loaded once per tile, read by both passes)
+  const bool regs = PM > 1 && (tile + BS - 1) / BS <= PM;
+  int A0 = klo == 0 ? 0 : sys_count_below(Pl[klo], U, N32);
+  for (int k = klo; k <= khi; ++k) {
+    const int A1 = k == G - 1 ? N32 : sys_count_below(Pl[k + 1], U, N32);
+    const int lo_w = max(A0, w0), hi_w = min(A1, w1);
+    if (lo_w < hi_w) {  // uniform
+      const int64_t s0 = (int64_t)k * tile;
+      const int len = (int)min((int64_t)tile, N - s0);
+      const int per = (len + BS - 1) / BS, j0 = t * per;
+      const double mk = rec_in[Rec<NX>::M * G + k];
+      const Real m = (Real)mk;
+      Real lv[PM];
+      double part = 0.0;
+      if (regs) {
+        load_tile_lw<Real, PM>(lw_in, N, tile, k, BS, lv);
+#pragma unroll
+        for (int q = 0; q < PM; ++q)
+          if (q < per && j0 + q < len) part += (lv[q] > -INFINITY) ? (double)exp_r<Real>(lv[q] - m) : 0.0;
+      } else {
+        for (int q = 0; q < per && j0 + q < len; ++q) {
+          const Real l = lw_in[s0 + j0 + q];
+          part += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
+        }
+      }
+      double tot;
+      double run = pblock_excl_scan<BS>(part, red, &tot);
+      if (ntiles++ == 0) PF_STAMP(7);
+      const double c = (mk > -INFINITY) ? exp(mk - h.M) / h.Sscan : 0.0;
+      const double base = Pl[k];
+      int before = -1;  // the last of this thread's particles that starts before slot lo_w
+      if (regs) {
+#pragma unroll
+        for (int q = 0; q < PM; ++q) {
+          if (q < per && j0 + q < len) {
+            const int L = sys_count_below(base + c * run, U, N32);
+            const int j = (int)s0 + j0 + q;
+            if (L < lo_w) before = j;
+            else if (L < hi_w) atomicMax(&anc_l[L - w0], j);
+            run += (lv[q] > -INFINITY) ? (double)exp_r<Real>(lv[q] - m) : 0.0;
+          }
+        }
+      } else {
+        for (int q = 0; q < per && j0 + q < len; ++q) {
+          const Real l = lw_in[s0 + j0 + q];
+          const int L = sys_count_below(base + c * run, U, N32);
+          const int j = (int)s0 + j0 + q;
+          if (L < lo_w) before = j;
+          else if (L < hi_w) atomicMax(&anc_l[L - w0], j);
+          run += (l > -INFINITY) ? (double)exp_r<Real>(l - m) : 0.0;
+        }
+      }
+      if (before >= 0) atomicMax(&anc_l[lo_w - w0], before);
+    }
+    A0 = A1;
+  }
+  PF_STAMP(8);
+#ifdef PF_STAMPS
+  if (stamp_on && t == 0 && blockIdx.y * gridDim.x + blockIdx.x < (unsigned)STAMP_WG)
+    g_pf_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * STAMP_SLOTS + 9] = (unsigned long long)ntiles;
+#endif
+  __syncthreads();
+  // fill: thread t owns slots [t pp, t pp + pp)
+  const int pp = (nsl + BS - 1) / BS, s0 = t * pp, s1 = min(s0 + pp, nsl);
+  int mx = -1;
+  for (int s = s0; s < s1; ++s) mx = max(mx, anc_l[s]);
+  mx = block_excl_max_i<BS>(mx, (int*)red);
+  for (int s = s0; s < s1; ++s) {
+    mx = max(mx, anc_l[s]);
+    anc_l[s] = mx;
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // Normals
 // ---------------------------------------------------------------------------
@@ -698,18 +850,17 @@ struct WAcc {
         for (int f = d; f < NX; ++f) s[c++] += e * x[d] * x[f];
     }
   }
-  // The thread's particles in one max-first pass (fp32 scalar state, 8 particles: chunk t, then
-  // chunk t + BS): no per-particle rescale.  Slots past the tile carry l = -inf, x = 0.
-  __device__ __forceinline__ void add_maxfirst8(const Real (&l)[8], const Real (&x)[8]) {
+  // The thread's particles (fp32 scalar state, 8 particles: chunk t, then chunk t + BS) relative to
+  // the workgroup's maximum M (block_max_f): every thread's sums share one reference, so the record
+  // merge is a plain sum (block_sum_lds) - no rescale factors, nothing rounded in fp32 beyond the
+  // per-particle exponentials.  Slots past the tile carry l = -inf, x = 0.
+  __device__ __forceinline__ void add_ref8(const Real (&l)[8], const Real (&x)[8], Real M) {
     static_assert(NX == 1, "scalar state");
-    Real mm = l[0];
-#pragma unroll
-    for (int e = 1; e < 8; ++e) mm = fmaxf(mm, l[e]);
-    m = mm;
-    if (!(mm > -INFINITY)) return;
+    m = M;
+    if (!(M > -INFINITY)) return;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const Real we = (l[e] > -INFINITY) ? exp_r<Real>(l[e] - mm) : Real(0);
+      const Real we = (l[e] > -INFINITY) ? exp_r<Real>(l[e] - M) : Real(0);
       s[0] += we;
       s[1] += we * we;
       s[2] += we * x[e];
@@ -752,9 +903,12 @@ struct WAcc {
   }
   // The same merge with one wave instead of all: every thread stages (m, s...) in LDS (stage:
   // [NS + 1][BS] floats), then wave 0 alone rescales and sums them - lane l takes threads l, l + 64,
-  // ... (fp32 rescale factors, fp64 sums), then one DPP sum per field.  The other waves do no
-  // reduction arithmetic at all.  The fp32 scalar step's default (PF_MERGE_LDS): sv64 306 -> 279
-  // us/step in a same-box A/B (profiles/r04/ab).
+  // ... with fp64 factors e^(m_t - M) relative to the wave's (= the workgroup's) maximum M and fp64
+  // sums, then one DPP sum per field.  The other waves do no reduction arithmetic at all.  The
+  // factors are fp64 exponentials (as in block_merge): with fp32 ones (~1e-7 relative) the tile
+  // records - the resampling CDF's tile masses - would carry fp32 rounding and a filter's ancestors
+  // would depend on how its particles are cut into tiles and shards.  The fp32 scalar step's default
+  // (PF_MERGE_LDS): sv64 306 -> 279 us/step in a same-box A/B (profiles/r04/ab).
   template <int BS>
   __device__ __forceinline__ void block_merge_lds(float* stage, double* out) {
     static_assert(sizeof(Real) == 4, "fp32 engine");
@@ -772,20 +926,41 @@ struct WAcc {
       mk[k] = stage[k * 64 + lane];
       Ml = fmaxf(Ml, mk[k]);
     }
+    const float Mw = wave_max_u(Ml);
     double acc[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) acc[i] = 0.0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const float f = (mk[k] > -INFINITY) ? __expf(mk[k] - Ml) : 0.0f;
+      const double f = (mk[k] > -INFINITY) ? exp((double)mk[k] - (double)Mw) : 0.0;
 #pragma unroll
-      for (int i = 0; i < NS; ++i) acc[i] = fma((double)stage[(1 + i) * BS + k * 64 + lane], (double)(i == 1 ? f * f : f), acc[i]);
+      for (int i = 0; i < NS; ++i) acc[i] = fma((double)stage[(1 + i) * BS + k * 64 + lane], i == 1 ? f * f : f, acc[i]);
     }
-    const float Mw = wave_max_u(Ml);
-    const double g = (Ml > -INFINITY) ? (double)__expf(Ml - Mw) : 0.0;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) out[1 + i] = wave_sum_ud(acc[i] * (i == 1 ? g * g : g));
+    for (int i = 0; i < NS; ++i) out[1 + i] = wave_sum_ud(acc[i]);
     out[0] = Mw;
+  }
+  // Merge of add_ref8 sums (one reference M for the whole workgroup): the partials staged in LDS,
+  // wave 0 sums them in fp64 (lane l: threads l, l + 64, ...), then one DPP sum per field.
+  template <int BS>
+  __device__ __forceinline__ void block_sum_lds(float* stage, double* out) {
+    static_assert(sizeof(Real) == 4, "fp32 engine");
+    constexpr int K = BS / 64;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) stage[i * BS + t] = s[i];
+    __syncthreads();
+    if (w != 0) return;
+    double acc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      acc[i] = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[i] += (double)stage[i * BS + k * 64 + lane];
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) out[1 + i] = wave_sum_ud(acc[i]);
+    out[0] = m;
   }
 };
 
@@ -921,7 +1096,7 @@ k_step(StepParams p) {
       }
 #pragma unroll
       for (int e = 0; e < SC; ++e) {
-        if (i0 + e < o1) {
+        if (CH == 4 || i0 + e < o1) {  // scalar state: slots past the tile computed too (padding, never used) - no per-slot branches
           if (p.do_predict) {
             M::transition(sx[e], P, u);
             M::add_lower(sx[e], sn[e], P, M::L::LQ);
@@ -930,17 +1105,20 @@ k_step(StepParams p) {
         }
       }
       if constexpr (FAST2) {
-        if (pre1 && p.do_predict && p.do_update == 1) {
+        if (pre1 && p.do_update == 1) {
           const int64_t i1 = o0 + (int64_t)(t + BS) * CH;
           Real n4[4];
-          chunk_normals4<Real>(p.seed, i1, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4,
-                               p.pbase);
+          if (p.do_predict)
+            chunk_normals4<Real>(p.seed, i1, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n4,
+                                 p.pbase);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {  // slots past o1 are never stored nor weighed
             Real xe[1] = {px[e]};
-            M::transition(xe, P, u);
-            Real ne[1] = {n4[e]};
-            M::add_lower(xe, ne, P, M::L::LQ);
+            if (p.do_predict) {
+              M::transition(xe, P, u);
+              Real ne[1] = {n4[e]};
+              M::add_lower(xe, ne, P, M::L::LQ);
+            }
             qx[e] = xe[0];
             qll[e] = M::loglik(xe, z, P, p.r_diag != 0);
           }
@@ -965,63 +1143,164 @@ k_step(StepParams p) {
   const bool gather = h.resample != 0;
   const double lprev_uniform = -log((double)p.N);
 
-  // ---- (1) ancestors of this thread's slots (thread-private LDS entries) ----
-  if (gather) {
-    if (p.method == 0) {
-      const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
-      int nextk = p.G;
-      for (int c = t; c < nchunks; c += BS) {
+  // ---- (2)+(3) per chunk: [gather + jitter] -> [predict] -> [weight] -> store
+  WA acc;
+  acc.init();
+  constexpr int NA = 1 + NX + RC::NC;  // aux: cnt, sum x, sum x x^T
+  double aux[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) aux[i] = 0.0;
+  const double lse_prev = h.uniform ? 0.0 : (p.use_lse_ext ? p.lse_ext : h.lse);  // shards: the global lse
+  const Real lse_r = (Real)lse_prev;
+  const bool write_x = p.do_predict || p.allow_gather;  // gather launches always produce x_out
+
+  bool fast = false, gfast = false;
+  // the generic chunk loop, instantiated for gathering and non-gathering workgroups apart: in the
+  // gathering one the speculated chunks are dead (fewer live registers through the ancestors)
+  auto chunk_loop = [&](auto gather_tag) {
+    constexpr bool gather_c = decltype(gather_tag)::value;
+    for (int c = t; c < nchunks; c += BS) {
+      const int64_t i0 = o0 + (int64_t)c * CH;
+      const bool first = PRE && c == t;
+      const bool spec = first && !gather_c;  // predicted x and loglik already computed
+      Real x[CH][NX];
+      Real lp[CH];
+      Real ll[CH];
+      if (gather_c) {
 #pragma unroll
         for (int e = 0; e < CH; ++e) {
-          const int64_t i = o0 + (int64_t)c * CH + e;
-          if (i < o1) {
-            const int k = prefix_tile(Pl, p.G, (U + (double)i) / (double)p.N);
-            anc_l[c * CH + e] = -1 - k;  // pending, in tile k
-            nextk = min(nextk, k);
+          const int a = (i0 + e < o1) ? anc_l[c * CH + e] : 0;
+#pragma unroll
+          for (int d = 0; d < NX; ++d) x[e][d] = x_in[(int64_t)d * p.Npad + a];
+          lp[e] = (Real)lprev_uniform;
+        }
+      } else {
+        Real lraw[CH];
+        if (spec) {
+#pragma unroll
+          for (int e = 0; e < CH; ++e) {
+#pragma unroll
+            for (int d = 0; d < NX; ++d) x[e][d] = sx[SC == CH ? e : 0][d];
+            lraw[e] = sl[SC == CH ? e : 0];
+            ll[e] = sll[SC == CH ? e : 0];
+          }
+        } else if constexpr (CH == 4) {
+          if (pre1 && c == t + BS) {  // prefetched before the prologue
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              x[e][0] = px[e];
+              lraw[e] = pl[e];
+            }
+          } else {
+            Real v[4];
+            load4<Real>(x_in + i0, v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e][0] = v[e];
+            if (p.do_update && !h.uniform) load4<Real>(lw_in + i0, lraw);
+          }
+        } else {
+#pragma unroll
+          for (int d = 0; d < NX; ++d) x[0][d] = x_in[(int64_t)d * p.Npad + i0];
+          if (p.do_update && !h.uniform) lraw[0] = lw_in[i0];
+        }
+        if (p.do_update) {
+#pragma unroll
+          for (int e = 0; e < CH; ++e)
+            lp[e] = h.uniform ? (Real)lprev_uniform : lraw[e] - lse_r;
+        }
+      }
+
+      Real nj4[CH], np4[CH];
+      if constexpr (CH == 4) {  // one Philox call covers the chunk's 4 scalar particles
+        if (gather_c && p.regularize)
+          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4, p.pbase);
+        if (p.do_predict) {
+          if (first) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) np4[e] = sn[e][0];
+          } else {
+            chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4,
+                                 p.pbase);
           }
         }
       }
-      int k = block_min_i<BS>(nextk, red);
-      // source tiles of <= 8 log-weights per thread: each tile's log-weights are loaded one tile
-      // ahead (the likeliest next source tile is k + 1), in flight through the current tile's
-      // searches, and read once (tile_cdf_regs) instead of twice from memory
-      constexpr int PM = sizeof(Real) == 4 ? 8 : 1;  // fp64: the 16 extra VGPRs would spill
-      const bool regs = PM > 1 && (p.tile + BS - 1) / BS <= PM;
-      Real lv[PM];
-      int kl = -1;
-      if (regs && k < p.G) {
-        load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k, BS, lv);
-        kl = k;
-      }
-      while (k < p.G) {
-        const int len = regs ? tile_cdf_regs<Real, NX, BS, PM>(lv, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red)
-                             : tile_cdf<Real, NX, BS>(lw_in, rec_in, p.G, p.N, p.tile, k, h, Pl, cdf, red);
-        if (regs && k + 1 < p.G) {
-          load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k + 1, BS, lv);
-          kl = k + 1;
-        }
-        nextk = p.G;
-        for (int c = t; c < nchunks; c += BS) {
 #pragma unroll
-          for (int e = 0; e < CH; ++e) {
-            const int64_t i = o0 + (int64_t)c * CH + e;
-            if (i < o1) {
-              const int a = anc_l[c * CH + e];
-              if (a == -1 - k) {
-                anc_l[c * CH + e] = (int)((int64_t)k * p.tile + lds_upper(cdf, len, (U + (double)i) / (double)p.N));
-              } else if (a < 0) {
-                nextk = min(nextk, -1 - a);
-              }
+      for (int e = 0; e < CH; ++e) {
+        const int64_t i = i0 + e;
+        if (i >= o1) break;
+        Real* xe = x[e];
+        if (gather_c) {
+          if (p.regularize) {
+            Real n[NX];
+            if constexpr (CH == 4) n[0] = nj4[e];
+            else fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n,
+                                        p.pbase);
+            M::add_lower(xe, n, P, M::L::LJ);
+          }
+          aux[0] += 1.0;
+#pragma unroll
+          for (int d = 0; d < NX; ++d) aux[1 + d] += (double)xe[d];
+          if constexpr (RC::COV) {
+            int cc = 1 + NX;
+#pragma unroll
+            for (int d = 0; d < NX; ++d)
+#pragma unroll
+              for (int f = d; f < NX; ++f) aux[cc++] += (double)xe[d] * (double)xe[f];
+          }
+        }
+        if (!spec) {
+          if (p.do_predict) {
+            Real n[NX];
+            if constexpr (CH == 4) {
+              n[0] = np4[e];
+            } else if (first) {
+#pragma unroll
+              for (int d = 0; d < NX; ++d) n[d] = sn[0][d];
+            } else {
+              fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n,
+                                     p.pbase);
+            }
+            M::transition(xe, P, u);
+            M::add_lower(xe, n, P, M::L::LQ);
+          }
+          ll[e] = (p.do_update == 1) ? M::loglik(xe, z, P, p.r_diag != 0) : Real(0);
+        }
+        if (p.do_update) {
+          lp[e] = lp[e] + ll[e];  // log(w_prev) - quad/2  (do_update == 2: reweigh only, ll = 0)
+          acc.add(lp[e], xe);
+        }
+      }
+      if constexpr (CH == 4) {
+        if (i0 + 3 < o1) {
+          if (write_x) {
+            Real v[4] = {x[0][0], x[1][0], x[2][0], x[3][0]};
+            store4<Real>(x_out + i0, v);
+          }
+          if (p.do_update) store4<Real>(lw_out + i0, lp);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (i0 + e < o1) {
+              if (write_x) x_out[i0 + e] = x[e][0];
+              if (p.do_update) lw_out[i0 + e] = lp[e];
             }
           }
         }
-        __syncthreads();  // the tile CDF is rebuilt for the next tile
-        k = block_min_i<BS>(nextk, red);
-        if (regs && k < p.G && k != kl) {
-          load_tile_lw<Real, PM>(lw_in, p.N, p.tile, k, BS, lv);
-          kl = k;
-        }
+      } else {
+        if (write_x)
+#pragma unroll
+          for (int d = 0; d < NX; ++d) x_out[(int64_t)d * p.Npad + i0] = x[0][d];
+        if (p.do_update) lw_out[i0] = lp[0];
       }
+    }
+  };
+
+  // ---- (1) ancestors of this thread's slots (LDS), then the chunks ----------
+  if (gather) {
+    if (p.method == 0) {
+      const double U = p.rp_unif ? p.rp_unif[r] : uniform53(p.seed, 0, rep, p.ep_resample);
+      constexpr int PM = sizeof(Real) == 4 ? 8 : 1;  // fp64: reloaded from L2 (registers)
+      sys_ancestors<Real, NX, BS, PM>(lw_in, rec_in, p.G, p.N, p.tile, o0, o1, U, h, Pl, anc_l, red, stamp_on);
     } else {  // multinomial: binary search of the materialised CDF (cdf /= cdf[-1])
       const double* C = p.cdf + (int64_t)r * p.N;
       const double last = C[p.N - 1];
@@ -1041,234 +1320,150 @@ k_step(StepParams p) {
         }
       }
     }
-  }
-  PF_STAMP(3);
-
-  // ---- (2)+(3) per chunk: [gather + jitter] -> [predict] -> [weight] -> store
-  WA acc;
-  acc.init();
-  constexpr int NA = 1 + NX + RC::NC;  // aux: cnt, sum x, sum x x^T
-  double aux[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) aux[i] = 0.0;
-  const double lse_prev = h.uniform ? 0.0 : (p.use_lse_ext ? p.lse_ext : h.lse);  // shards: the global lse
-  const Real lse_r = (Real)lse_prev;
-  const bool write_x = p.do_predict || p.allow_gather;  // gather launches always produce x_out
-
-  // fast finish of the fp32 scalar step (uniform per workgroup): every chunk of the thread was
-  // speculated and nothing is gathered
-  bool fast = false;
-  if constexpr (FAST2) {
-#ifndef PF_NO_PRE1
-    constexpr int SPEC_CHUNKS = 2;
-#else
-    constexpr int SPEC_CHUNKS = 1;
+    PF_STAMP(3);
+    // gather-fast (fp32 scalar, <= 2 chunks per thread, fused predict + update after a resample): the
+    // thread's 8 gathered slots straight through, weighed against the workgroup maximum as the fast
+    // path does - so this step and the same step run as a gather-only launch followed by a fast launch
+    // (a run cut at a resample) give bitwise the same records
+    if constexpr (FAST2) {
+#ifndef PF_GFAST
+#define PF_GFAST 1
 #endif
-    fast = !gather && p.do_predict && p.do_update == 1 && nchunks <= SPEC_CHUNKS * BS;
-    if (fast && t < nchunks) {
-      const Real lu = (Real)lprev_uniform;
-      const int64_t ia = o0 + (int64_t)t * CH, ib = o0 + (int64_t)(t + BS) * CH;
-      const int na = (int)min((int64_t)4, o1 - ia), nb = spec1 ? (int)min((int64_t)4, o1 - ib) : 0;
-      Real lp[8], xv[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xv[e] = e < na ? sx[e][0] : Real(0);  // slots past the tile: zero weight, finite value
-        lp[e] = e < na ? (h.uniform ? lu : sl[e] - lse_r) + sll[e] : -INFINITY;
-        xv[4 + e] = e < nb ? qx[e] : Real(0);
-        lp[4 + e] = e < nb ? (h.uniform ? lu : pl[e] - lse_r) + qll[e] : -INFINITY;
-      }
-      // max-first over the thread's 8 particles - the same pass the generic loop makes for this
-      // geometry (klp / kx below), so a step computed here and the same step computed there (e.g.
-      // after an in-kernel gather) give bitwise the same records: a run cut into segments stays
-      // bitwise the uninterrupted run
-      acc.add_maxfirst8(lp, xv);
-      if (na == 4) {
-        store4<Real>(x_out + ia, xv);
-        store4<Real>(lw_out + ia, lp);
-      } else {
-        for (int e = 0; e < na; ++e) {
-          x_out[ia + e] = xv[e];
-          lw_out[ia + e] = lp[e];
-        }
-      }
-      if (nb == 4) {
-        store4<Real>(x_out + ib, xv + 4);
-        store4<Real>(lw_out + ib, lp + 4);
-      } else {
-        for (int e = 0; e < nb; ++e) {
-          x_out[ib + e] = xv[4 + e];
-          lw_out[ib + e] = lp[4 + e];
-        }
-      }
-    }
-  }
-
-  // generic loop in the fast path's geometry (<= 2 chunks per thread, fp32 scalar): the particles are
-  // kept and accumulated max-first after the loop, exactly as the fast path does
-  bool fastgeo = false;
-  Real klp[QC * 2], kx[QC * 2];
-  if constexpr (FAST2) {
-#ifndef PF_NO_PRE1
-    fastgeo = nchunks <= 2 * BS;
-#else
-    fastgeo = nchunks <= BS;
-#endif
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      klp[e] = -INFINITY;
-      kx[e] = Real(0);
-    }
-  }
-  for (int c = t; c < (fast ? 0 : nchunks); c += BS) {
-    const int64_t i0 = o0 + (int64_t)c * CH;
-    const bool first = PRE && c == t;
-    const bool spec = first && !gather;  // predicted x and loglik already computed
-    Real x[CH][NX];
-    Real lp[CH];
-    Real ll[CH];
-    if (gather) {
-#pragma unroll
-      for (int e = 0; e < CH; ++e) {
-        const int a = (i0 + e < o1) ? anc_l[c * CH + e] : 0;
-#pragma unroll
-        for (int d = 0; d < NX; ++d) x[e][d] = x_in[(int64_t)d * p.Npad + a];
-        lp[e] = (Real)lprev_uniform;
-      }
-    } else {
-      Real lraw[CH];
-      if (spec) {
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-#pragma unroll
-          for (int d = 0; d < NX; ++d) x[e][d] = sx[SC == CH ? e : 0][d];
-          lraw[e] = sl[SC == CH ? e : 0];
-          ll[e] = sll[SC == CH ? e : 0];
-        }
-      } else if constexpr (CH == 4) {
-        if (pre1 && c == t + BS) {  // prefetched before the prologue
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x[e][0] = px[e];
-            lraw[e] = pl[e];
-          }
-        } else {
-          Real v[4];
-          load4<Real>(x_in + i0, v);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x[e][0] = v[e];
-          if (p.do_update && !h.uniform) load4<Real>(lw_in + i0, lraw);
-        }
-      } else {
-#pragma unroll
-        for (int d = 0; d < NX; ++d) x[0][d] = x_in[(int64_t)d * p.Npad + i0];
-        if (p.do_update && !h.uniform) lraw[0] = lw_in[i0];
-      }
-      if (p.do_update) {
-#pragma unroll
-        for (int e = 0; e < CH; ++e)
-          lp[e] = h.uniform ? (Real)lprev_uniform : lraw[e] - lse_r;
-      }
-    }
-
-    Real nj4[CH], np4[CH];
-    if constexpr (CH == 4) {  // one Philox call covers the chunk's 4 scalar particles
-      if (gather && p.regularize)
-        chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, nj4, p.pbase);
-      if (p.do_predict) {
-        if (first) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) np4[e] = sn[e][0];
-        } else {
-          chunk_normals4<Real>(p.seed, i0, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, np4,
-                               p.pbase);
-        }
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      const int64_t i = i0 + e;
-      if (i >= o1) break;
-      Real* xe = x[e];
-      if (gather) {
-        if (p.regularize) {
-          Real n[NX];
-          if constexpr (CH == 4) n[0] = nj4[e];
-          else fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, n,
-                                      p.pbase);
-          M::add_lower(xe, n, P, M::L::LJ);
-        }
-        aux[0] += 1.0;
-#pragma unroll
-        for (int d = 0; d < NX; ++d) aux[1 + d] += (double)xe[d];
-        if constexpr (RC::COV) {
-          int cc = 1 + NX;
-#pragma unroll
-          for (int d = 0; d < NX; ++d)
-#pragma unroll
-            for (int f = d; f < NX; ++f) aux[cc++] += (double)xe[d] * (double)xe[f];
-        }
-      }
-      if (!spec) {
-        if (p.do_predict) {
-          Real n[NX];
-          if constexpr (CH == 4) {
-            n[0] = np4[e];
-          } else if (first) {
-#pragma unroll
-            for (int d = 0; d < NX; ++d) n[d] = sn[0][d];
-          } else {
-            fill_normals<NX, Real>(p.seed, i, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, n,
-                                   p.pbase);
-          }
-          M::transition(xe, P, u);
-          M::add_lower(xe, n, P, M::L::LQ);
-        }
-        ll[e] = (p.do_update == 1) ? M::loglik(xe, z, P, p.r_diag != 0) : Real(0);
-      }
-      if (p.do_update) {
-        lp[e] = lp[e] + ll[e];  // log(w_prev) - quad/2  (do_update == 2: reweigh only, ll = 0)
-        if constexpr (FAST2) {
-          if (fastgeo) {
-            if (c == t) {
-              klp[e] = lp[e];
-              kx[e] = xe[0];
-            } else {
-              klp[4 + e] = lp[e];
-              kx[4 + e] = xe[0];
-            }
-          } else {
-            acc.add(lp[e], xe);
-          }
-        } else {
-          acc.add(lp[e], xe);
-        }
-      }
-    }
-    if constexpr (CH == 4) {
-      if (i0 + 3 < o1) {
-        if (write_x) {
-          Real v[4] = {x[0][0], x[1][0], x[2][0], x[3][0]};
-          store4<Real>(x_out + i0, v);
-        }
-        if (p.do_update) store4<Real>(lw_out + i0, lp);
-      } else {
+      gfast = PF_GFAST && gather && p.do_predict && p.do_update == 1 && nchunks <= 2 * BS;
+      Real xv[8], lp[8];
+      float mt = -INFINITY;  // this thread's maximum log-weight
+      if (gfast && t < nchunks) {
+        const int ca = t, cb = t + BS;
+        const int64_t ia = o0 + (int64_t)ca * CH, ib = o0 + (int64_t)cb * CH;
+        const int na = (int)min((int64_t)4, o1 - ia), nb = cb < nchunks ? (int)min((int64_t)4, o1 - ib) : 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (i0 + e < o1) {
-            if (write_x) x_out[i0 + e] = x[e][0];
-            if (p.do_update) lw_out[i0 + e] = lp[e];
+          xv[e] = e < na ? x_in[anc_l[ca * CH + e]] : Real(0);
+          xv[4 + e] = e < nb ? x_in[anc_l[cb * CH + e]] : Real(0);
+        }
+        if (p.regularize) {
+          Real ja[4], jb[4];
+          chunk_normals4<Real>(p.seed, ia, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, ja, p.pbase);
+          if (nb > 0)
+            chunk_normals4<Real>(p.seed, ib, (uint32_t)r, rep, p.ep_resample, STREAM_JITTER, p.rp_jit, p.N, jb, p.pbase);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            Real xa[1] = {xv[e]}, na1[1] = {ja[e]};
+            M::add_lower(xa, na1, P, M::L::LJ);
+            xv[e] = xa[0];
+            if (nb > 0) {
+              Real xb[1] = {xv[4 + e]}, nb1[1] = {jb[e]};
+              M::add_lower(xb, nb1, P, M::L::LJ);
+              xv[4 + e] = xb[0];
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // the generic loop's order: chunk t's slots, then chunk t + BS's
+          if (e < na || (e >= 4 && e - 4 < nb)) {
+            aux[0] += 1.0;
+            aux[1] += (double)xv[e];
+            if constexpr (RC::COV) aux[2] += (double)xv[e] * (double)xv[e];
+          }
+        }
+        Real pb[4];
+        if (nb > 0)
+          chunk_normals4<Real>(p.seed, ib, (uint32_t)r, rep, p.ep_predict, STREAM_PROCESS, p.rp_noise, p.N, pb, p.pbase);
+        const Real lu = (Real)lprev_uniform;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool in = e < 4 ? e < na : e - 4 < nb;
+          Real xe[1] = {xv[e]};
+          Real ne[1] = {e < 4 ? sn[e][0] : pb[e - 4]};
+          M::transition(xe, P, u);
+          M::add_lower(xe, ne, P, M::L::LQ);
+          xv[e] = in ? xe[0] : Real(0);
+          lp[e] = in ? lu + M::loglik(xe, z, P, p.r_diag != 0) : -INFINITY;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mt = fmaxf(mt, lp[e]);
+        if (na == 4) {
+          store4<Real>(x_out + ia, xv);
+          store4<Real>(lw_out + ia, lp);
+        } else {
+          for (int e = 0; e < na; ++e) {
+            x_out[ia + e] = xv[e];
+            lw_out[ia + e] = lp[e];
+          }
+        }
+        if (nb == 4) {
+          store4<Real>(x_out + ib, xv + 4);
+          store4<Real>(lw_out + ib, lp + 4);
+        } else {
+          for (int e = 0; e < nb; ++e) {
+            x_out[ib + e] = xv[4 + e];
+            lw_out[ib + e] = lp[4 + e];
           }
         }
       }
-    } else {
-      if (write_x)
-#pragma unroll
-        for (int d = 0; d < NX; ++d) x_out[(int64_t)d * p.Npad + i0] = x[0][d];
-      if (p.do_update) lw_out[i0] = lp[0];
+      if (gfast) {  // uniform: the workgroup's reference maximum, then the thread's sums against it
+        const float Mb = block_max_f<BS>(mt, (float*)(cdf + 32));  // the merge staging area: free here
+        if (t < nchunks) acc.add_ref8(lp, xv, Mb);
+      }
     }
-  }
-  if constexpr (FAST2) {
-    if (fastgeo && !fast && p.do_update && t < nchunks) acc.add_maxfirst8(klp, kx);
+    if (!gfast) chunk_loop(std::true_type{});
+  } else {
+    PF_STAMP(3);
+    // fast finish of the fp32 scalar step (uniform per workgroup): every chunk of the thread was
+    // speculated and nothing is gathered
+    if constexpr (FAST2) {
+#ifndef PF_NO_PRE1
+      constexpr int SPEC_CHUNKS = 2;
+#else
+      constexpr int SPEC_CHUNKS = 1;
+#endif
+      fast = !gather && p.do_update == 1 && nchunks <= SPEC_CHUNKS * BS;  // fused step, or update only
+      Real lp[8], xv[8];
+      float mt = -INFINITY;  // this thread's maximum log-weight
+      if (fast && t < nchunks) {
+        const Real lu = (Real)lprev_uniform;
+        const int64_t ia = o0 + (int64_t)t * CH, ib = o0 + (int64_t)(t + BS) * CH;
+        const int na = (int)min((int64_t)4, o1 - ia), nb = spec1 ? (int)min((int64_t)4, o1 - ib) : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // arithmetic on every slot, then selects (no per-slot branches)
+          const Real va = (h.uniform ? lu : sl[e] - lse_r) + sll[e];
+          const Real vb = (h.uniform ? lu : pl[e] - lse_r) + qll[e];
+          xv[e] = e < na ? sx[e][0] : Real(0);  // slots past the tile: zero weight, finite value
+          lp[e] = e < na ? va : -INFINITY;
+          xv[4 + e] = e < nb ? qx[e] : Real(0);
+          lp[4 + e] = e < nb ? vb : -INFINITY;
+        }
+        // the weights against the workgroup's maximum (add_ref8) - the same pass the gather-fast block
+        // makes, so a step after a gather-only launch (a run cut at a resample) and the same step fused
+        // with its gather give bitwise the same records: a run cut into segments stays the uninterrupted run
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mt = fmaxf(mt, lp[e]);
+        if (na == 4) {
+          if (write_x) store4<Real>(x_out + ia, xv);
+          store4<Real>(lw_out + ia, lp);
+        } else {
+          for (int e = 0; e < na; ++e) {
+            if (write_x) x_out[ia + e] = xv[e];
+            lw_out[ia + e] = lp[e];
+          }
+        }
+        if (nb == 4) {
+          if (write_x) store4<Real>(x_out + ib, xv + 4);
+          store4<Real>(lw_out + ib, lp + 4);
+        } else {
+          for (int e = 0; e < nb; ++e) {
+            if (write_x) x_out[ib + e] = xv[4 + e];
+            lw_out[ib + e] = lp[4 + e];
+          }
+        }
+      }
+      if (fast) {  // uniform
+        const float Mb = block_max_f<BS>(mt, (float*)(cdf + 32));  // the merge staging area: free here
+        if (t < nchunks) acc.add_ref8(lp, xv, Mb);
+      }
+    }
+
+    if (!fast) chunk_loop(std::false_type{});
   }
   PF_STAMP(4);
 
@@ -1282,7 +1477,8 @@ k_step(StepParams p) {
 #if PF_MERGE_LDS
     if constexpr (NX == 1 && sizeof(Real) == 4) {  // staged after the record's slots (step_lds: MERGE_LDS_BYTES)
       static_assert((WA::NS + 1) * BS * 4 + 32 * 8 <= MERGE_LDS_BYTES && RC::SIZE <= 32, "merge staging");
-      acc.template block_merge_lds<BS>((float*)(cdf + 32), w);
+      if (fast || gfast) acc.template block_sum_lds<BS>((float*)(cdf + 32), w);  // one reference maximum
+      else acc.template block_merge_lds<BS>((float*)(cdf + 32), w);
     }
     else
 #endif
