@@ -866,7 +866,9 @@ def main():
     achieved = alg_bytes_run / (device_ms_step * 1e-3) / 1e9
     dyn = lib.pf_kernel_path(pf.handle) == NV.PF_PATH_RUNTIME
     # large states: group kernel; shapes outside the compiled list: the runtime-shape kernel
-    kname = "k_resident" if resident else ("k_dyn_step" if dyn else ("k_step_grp" if nx >= 16 else "k_step"))
+    streamed = bool(lib.pf_last_step_streamed(pf.handle))  # persistent many-replicate step (k_step_stream)
+    kname = "k_resident" if resident else ("k_dyn_step" if dyn else ("k_step_grp" if nx >= 16 else
+                                                                    ("k_step_stream" if streamed else "k_step")))
     ktmpl = wl.kernel_tmpl.split(",", 1)[1]
     if dyn:
         ktmpl = ",".join(ktmpl.split(",")[-2:])  # k_dyn_step<Real, TK, OK>
@@ -973,7 +975,8 @@ def main():
                          # the HBM fraction on the bytes the counters saw move (FETCH x2 + WRITE per step)
                          "traffic_gbs": None if traffic is None else traffic / step_s / 1e9,
                          "traffic_frac": None if traffic is None else traffic / step_s / 1e9 / HBM_PEAK_GBS,
-                         "kernel": f"pf::{kname}<{real},{ktmpl}>",
+                         "kernel": (f"pf::{kname}<{','.join(ktmpl.split(',')[1:])}>" if streamed
+                                    else f"pf::{kname}<{real},{ktmpl}>"),
                          "steps_per_launch": K if resident else 1,
                          "algorithmic_bytes_per_step": alg_bytes_run / K,
                          "algorithmic_bytes_per_launch": alg_bytes_run / (1 if resident else K),

@@ -108,6 +108,9 @@ int32_t pf_model_supported(int32_t nx, int32_t nz, int32_t trans_kind, int32_t o
 int32_t pf_model_compiled(int32_t nx, int32_t nz, int32_t trans_kind, int32_t obs_kind);
 /* PF_PATH_RUNTIME if the handle runs the runtime-shape kernels, else PF_PATH_AUTO. */
 int32_t pf_kernel_path(pf_handle* h);
+/* 1 if the handle's last fused step launch ran the persistent many-replicate kernel (k_step_stream:
+ * fp32 scalar models with per-step replicate heads; PF_STREAM=0 turns it off), else 0.  Diagnostics. */
+int32_t pf_last_step_streamed(pf_handle* h);
 
 /* initialize (pf.py:110-132): particles ~ N(mean_r, cov_r), uniform weights.
  * mean [R][nx], cov [R][nx][nx]; replay_normals [R][N][nx] or NULL (device Philox). */

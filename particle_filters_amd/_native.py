@@ -105,6 +105,7 @@ SIGNATURES = {
     "pf_model_supported": (C.c_int32, [C.c_int32] * 4),
     "pf_model_compiled": (C.c_int32, [C.c_int32] * 4),
     "pf_kernel_path": (C.c_int32, [_vp]),
+    "pf_last_step_streamed": (C.c_int32, [_vp]),
     "pf_create": (C.c_int32, [C.POINTER(ModelDesc), C.POINTER(Opts), C.POINTER(_vp)]),
     "pf_destroy": (None, [_vp]),
     "pf_initialize": (C.c_int32, [_vp, _dp, _dp, _dp]),

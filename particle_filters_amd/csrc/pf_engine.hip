@@ -194,6 +194,9 @@ struct pf_handle {
   bool cdf_needed() const { return needs_cdf() && !(lcum_mode && lcum_valid && method == 0 && !sharded); }
   // per-step replicate heads (k_head, StepParams::head): -1 auto, 0 off, 1 on (PF_HEAD)
   int head_mode = -1;
+  // persistent fused step for head launches of the fp32 scalar models (k_step_stream): 1 on, 0 off (PF_STREAM)
+  int stream_mode = 1;
+  bool last_stream = false;  // the last fused step launch ran k_step_stream
   double* head = nullptr;  // [R][HEAD_STRIDE]
   // the launch that produced the current heads (reused by the next launch when equal)
   bool head_valid = false;
@@ -436,8 +439,20 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
   const bool use_lcum = h->lcum_mode && !h->sharded && h->method == 0;
   p.lcum_in = (use_lcum && h->lcum_valid && p.allow_gather) ? h->lcum[h->clcum] : nullptr;
   p.lcum_out = (use_lcum && p.do_update) ? h->lcum[h->clcum ^ 1] : nullptr;
-  dim3 grid((unsigned)h->G, (unsigned)h->R);
-  HIPCHK(h->ops->step(p, grid, step_lds(h, p.allow_gather != 0), h->stream));
+  // the fused many-replicate fp32 scalar step: the persistent kernel (its paths need the heads, the
+  // systematic method, <= 2 chunks of 4 per thread and the state in the record)
+  const bool stream = h->stream_mode && h->ops->stream && p.head && p.do_predict && p.do_update == 1 &&
+                      p.method == 0 && h->tile <= 2048 && h->tile >= 512 && h->R <= 1024 && !p.use_lse_ext &&
+                      !p.xr_out && !p.anc_out;
+  if (p.do_predict && p.do_update == 1) h->last_stream = stream;
+  if (stream) {  // LDS: k_step's gather layout + the replicates' decisions (R ints after the ancestors)
+    const size_t smem = base_lds_bytes(h->G) + (size_t)h->tile * (sizeof(double) + sizeof(int)) +
+                        (((size_t)h->R * sizeof(int) + 15) & ~(size_t)15);
+    HIPCHK(h->ops->stream(p, h->R, std::max(smem, step_lds(h, true)), h->stream));
+  } else {
+    dim3 grid((unsigned)h->G, (unsigned)h->R);
+    HIPCHK(h->ops->step(p, grid, step_lds(h, p.allow_gather != 0), h->stream));
+  }
   if (p.lcum_out) h->clcum ^= 1;
   // the prefix describes exactly the weights an update launch wrote
   if (writes_lw || p.allow_gather) h->lcum_valid = p.lcum_out != nullptr;
@@ -898,6 +913,7 @@ int32_t pf_model_compiled(int32_t nx, int32_t nz, int32_t tk, int32_t ok) {
 }
 
 int32_t pf_kernel_path(pf_handle* h) { return (h && h->ops && h->ops->dyn) ? PF_PATH_RUNTIME : PF_PATH_AUTO; }
+int32_t pf_last_step_streamed(pf_handle* h) { return (h && h->last_stream) ? 1 : 0; }
 
 pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
   if (!m || !o || !out) return fail(PF_E_ARG, "null argument");
@@ -1077,6 +1093,7 @@ pf_status pf_create(const pf_model_desc* m, const pf_opts* o, pf_handle** out) {
       if (hipMalloc((void**)&h->lcum[k], (size_t)h->R * h->N * sizeof(double)) != hipSuccess)
         return cleanup(fail(PF_E_HIP, "hipMalloc of the CDF prefix failed"));
   if (const char* he = std::getenv("PF_HEAD")) h->head_mode = std::atoi(he) != 0 ? 1 : 0;
+  if (const char* se = std::getenv("PF_STREAM")) h->stream_mode = std::atoi(se) != 0 ? 1 : 0;
   if (hipMalloc((void**)&h->head, (size_t)h->R * HEAD_STRIDE * sizeof(double)) != hipSuccess)
     return cleanup(fail(PF_E_HIP, "hipMalloc of replicate heads failed"));
   if (h->wrows > 0 && hipMalloc(&h->wbuf, (size_t)h->R * h->wrows * h->Npad * h->esz) != hipSuccess)

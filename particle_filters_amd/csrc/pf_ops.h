@@ -13,6 +13,7 @@
 #include "pf_resident.h"
 #include "pf_shard_kernels.h"
 #include "pf_step_grp.h"
+#include "pf_step_stream.h"
 
 namespace pf {
 
@@ -36,6 +37,9 @@ struct Ops {
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
   // cannot be co-resident (the caller then runs the launch-per-step path).
   hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t, bool coop);
+  // persistent fused step of the many-replicate fp32 scalar launches (pf_step_stream.h; null otherwise):
+  // grid = min(G R, co-resident workgroups), tiles walked with the next tile's operands in flight
+  hipError_t (*stream)(const StepParams&, int R, size_t smem, hipStream_t);
   int (*resident_cap)();  // workgroups of k_resident co-resident on the current device (0: unknown)
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
@@ -131,6 +135,7 @@ struct Launch {
     o.prepare = &prepare;
     o.resident = nullptr;
     o.resident_cap = nullptr;
+    o.stream = nullptr;
     o.shard_offspring = &shard_offspring;
     o.shard_adopt = &shard_adopt;
     return o;
@@ -200,12 +205,42 @@ struct ResidentLaunch {
   static int cap() { return cap_of<false>(); }
 };
 
+template <int NZ, int TK, int OK>
+struct StreamLaunch {
+  // one workgroup per co-resident slot (CUs x the occupancy API, cached per device and LDS size), at
+  // most one per tile; no workgroup waits for another, so any grid is correct
+  static hipError_t launch(const StepParams& p, int R, size_t smem, hipStream_t s) {
+    static int cached_dev = -1, cached_cap = 0;
+    static size_t cached_smem = 0;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev != cached_dev || smem != cached_smem) {
+      int cus = 0, per_cu = 0;
+      (void)hipFuncSetAttribute((const void*)k_step_stream<NZ, TK, OK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+      if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_step_stream<NZ, TK, OK>, 256,
+                                                            smem)) != hipSuccess)
+        return e;
+      cached_dev = dev;
+      cached_smem = smem;
+      cached_cap = cus * (per_cu > 0 ? per_cu : 1);
+    }
+    const long long ntiles = (long long)p.G * R;
+    const unsigned grid = (unsigned)(ntiles < cached_cap ? ntiles : cached_cap);
+    hipLaunchKernelGGL((k_step_stream<NZ, TK, OK>), dim3(grid), dim3(256), smem, s, p, R);
+    return hipGetLastError();
+  }
+};
+
 template <int NX, int NZ, int TK, int OK>
 inline void register_both() {
   Ops f32 = Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32);
   if constexpr (NX == 1) {
     f32.resident = &ResidentLaunch<NX, NZ, TK, OK>::launch;
     f32.resident_cap = &ResidentLaunch<NX, NZ, TK, OK>::cap;
+    f32.stream = &StreamLaunch<NZ, TK, OK>::launch;
   }
   register_ops(f32);
   register_ops(Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64));

@@ -1,0 +1,86 @@
+"""Fold the PMC passes of tools/gpu_pmc_all.sh into profiles/pmc_*.json (read by bench.py) and copy
+the raw counter files under profiles/r04/pmc/.
+
+    python tools/pmc_fold_r04.py gpurun_out/<pmc dir>
+
+Per workload: FETCH_SIZE / WRITE_SIZE per launch of the bench line's dominant kernel (separate
+passes, tools/pmc_summary.py: KiB -> B, FETCH doubled on gfx950), summed over its launches and
+divided by the filter steps the profiled bench run covers (warm-up + timed: W + K, the convention of
+the earlier rounds' summaries); the SQ issue counters through tools/pmc_valu.py."""
+import csv
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+D = sys.argv[1]
+OUT = os.path.join(REPO, "profiles", "r04", "pmc")
+os.makedirs(OUT, exist_ok=True)
+
+# name: (bench steps K, warm-up W, kernel substring, kernel_short, steps per launch for pmc_valu, SIMDs)
+LINES = {
+    "sv": (20, 5, "k_resident<float, 1, 1", "k_resident", 20, None),
+    "sv64": (20, 3, "k_step_stream<1, 0, 0>", "k_step_stream", 1, 1024),
+    "sv_fp64": (20, 5, "k_step<double, 1, 1", "k_step", 1, 1024),
+    "l96": (50, 5, "k_step_grp<float, 40, 10", "k_step_grp", 1, 1024),
+    "mat": (40, 4, "k_step_grp<float, 16, 25", "k_step_grp", 1, 1024),
+    "ledh": (50, 5, "k_ledh_fused", "k_ledh_fused", 1, 1024),
+}
+OUTNAME = {"sv": "pmc_traffic.json"}
+
+
+def first(pattern):
+    g = sorted(glob.glob(pattern, recursive=True))
+    return g[0] if g else None
+
+
+def launches(path, counter, kern):
+    return sum(1 for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"] and r["Counter_Name"] == counter)
+
+
+for name, (K, W, kern, short, spl, simds) in LINES.items():
+    fcsv = first(f"{D}/{name}_FETCH_SIZE/**/*counter_collection.csv")
+    wcsv = first(f"{D}/{name}_WRITE_SIZE/**/*counter_collection.csv")
+    if not (fcsv and wcsv):
+        print(f"{name}: no traffic passes under {D}")
+        continue
+    dst_f = os.path.join(OUT, f"{name}_FETCH_SIZE_counter_collection.csv")
+    dst_w = os.path.join(OUT, f"{name}_WRITE_SIZE_counter_collection.csv")
+    shutil.copy(fcsv, dst_f)
+    shutil.copy(wcsv, dst_w)
+    n = launches(dst_f, "FETCH_SIZE", kern)
+    steps = W + K
+    print(f"{name}: {n} launches of {kern}, {steps} filter steps")
+    rel_f, rel_w = os.path.relpath(dst_f, REPO), os.path.relpath(dst_w, REPO)
+    out = os.path.join(REPO, "profiles", OUTNAME.get(name, f"pmc_traffic_{name}.json"))
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), rel_f, rel_w, kern, str(steps), out,
+                    short], check=True, cwd=REPO, stdout=subprocess.DEVNULL)
+    db = first(f"{D}/{name}_issue/**/*results.db")
+    if db:
+        # per-dispatch counter sums exported as CSV (the rocpd database itself is ~5 MB)
+        import sqlite3
+        c = sqlite3.connect(db)
+        rows = c.execute("select dispatch_id, kernel_name, counter_name, sum(value) from counters_collection "
+                         "group by dispatch_id, counter_name order by dispatch_id").fetchall()
+        dst_csv = os.path.join(OUT, f"{name}_issue_counters.csv")
+        with open(dst_csv, "w", newline="") as fh:
+            wr = csv.writer(fh)
+            wr.writerow(["dispatch_id", "kernel_name", "counter_name", "value"])
+            wr.writerows(rows)
+        # the resident kernel occupies 4 SIMDs per workgroup of its grid: pmc_valu takes the grid's SIMDs
+        sim = simds if simds else int(os.environ.get("PF_RES_SIMDS", "980"))
+        outj = os.path.join(REPO, "profiles", f"pmc_valu_{name}.json")
+        subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_valu.py"), db, name, short, str(spl), str(sim),
+                        outj], check=True, cwd=REPO, stdout=subprocess.DEVNULL)
+        import json
+        d = json.load(open(outj))
+        d["source"] = (f"rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES "
+                       f"({name}); 2 cycles per wave VALU issue, 2.4 GHz; per-dispatch sums in "
+                       f"{os.path.relpath(dst_csv, REPO)} (tools/gpu_pmc_all.sh, tools/pmc_fold_r04.py)")
+        json.dump(d, open(outj, "w"), indent=1)
+    st = first(f"{D}/{name}_stats/**/*kernel_stats.csv")
+    if st:
+        shutil.copy(st, os.path.join(OUT, f"{name}_kernel_stats.csv"))
+print("folded into profiles/pmc_*.json; raw files under profiles/r04/pmc/")
