@@ -156,15 +156,15 @@ k_step_stream(StepParams p, int R) {
   // ---- pass 1: replicates that did not resample, the next tile's operands in flight --------
   StreamPre<NZ> cur;
   int id = blockIdx.x;
-  if (id < ntiles) stream_fetch<BS, NZ>(p, id, cur);
   __syncthreads();  // flags
+  if (id < ntiles && !flags[id / G]) stream_fetch<BS, NZ>(p, id, cur);
   int ngather = 0;
   for (; id < ntiles; id += gridDim.x) {  // uniform per workgroup
     const StepParams& q = p;
     const int r = id / G, b = id - r * G;
     StreamPre<NZ> nxt;
     const int nid = id + gridDim.x;
-    if (nid < ntiles) stream_fetch<BS, NZ>(q, nid, nxt);
+    if (nid < ntiles && !flags[nid / G]) stream_fetch<BS, NZ>(q, nid, nxt);  // (a gathering tile reads its own)
     if (flags[r]) {  // pass 2
       ++ngather;
       cur = nxt;
