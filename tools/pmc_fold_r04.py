@@ -5,8 +5,8 @@ the raw counter files under profiles/r04/pmc/.
 
 Per workload: FETCH_SIZE / WRITE_SIZE per launch of the bench line's dominant kernel (separate
 passes, tools/pmc_summary.py: KiB -> B, FETCH doubled on gfx950), summed over its launches and
-divided by the filter steps the profiled bench run covers (warm-up + timed: W + K, the convention of
-the earlier rounds' summaries); the SQ issue counters through tools/pmc_valu.py."""
+divided by the filter steps the profiled bench run covers (STEPS below); the SQ issue counters
+through tools/pmc_valu.py."""
 import csv
 import glob
 import os
@@ -19,6 +19,9 @@ D = sys.argv[1]
 OUT = os.path.join(REPO, "profiles", "r04", "pmc")
 os.makedirs(OUT, exist_ok=True)
 
+# filter steps the profiled bench run covers: the warm-up W and the timed K, plus (nx > 4 with the
+# covariance) a second K-step window for the step kernels' own time, or (LEDH) a second W + K run
+STEPS = {"l96": lambda K, W: W + 2 * K, "mat": lambda K, W: W + 2 * K, "ledh": lambda K, W: 2 * (W + K)}
 # name: (bench steps K, warm-up W, kernel substring, kernel_short, steps per launch for pmc_valu, SIMDs)
 LINES = {
     "sv": (20, 5, "k_resident<float, 1, 1", "k_resident", 20, None),
@@ -26,7 +29,7 @@ LINES = {
     "sv_fp64": (20, 5, "k_step<double, 1, 1", "k_step", 1, 1024),
     "l96": (50, 5, "k_step_grp<float, 40, 10", "k_step_grp", 1, 1024),
     "mat": (40, 4, "k_step_grp<float, 16, 25", "k_step_grp", 1, 1024),
-    "ledh": (50, 5, "k_ledh_fused", "k_ledh_fused", 1, 1024),
+    "ledh": (50, 5, "k_ledh_fused", "k_ledh_fused", 1, 628),  # 157 one-wave-per-SIMD workgroups
 }
 OUTNAME = {"sv": "pmc_traffic.json"}
 
@@ -51,7 +54,7 @@ for name, (K, W, kern, short, spl, simds) in LINES.items():
     shutil.copy(fcsv, dst_f)
     shutil.copy(wcsv, dst_w)
     n = launches(dst_f, "FETCH_SIZE", kern)
-    steps = W + K
+    steps = STEPS.get(name, lambda K, W: W + K)(K, W)
     print(f"{name}: {n} launches of {kern}, {steps} filter steps")
     rel_f, rel_w = os.path.relpath(dst_f, REPO), os.path.relpath(dst_w, REPO)
     out = os.path.join(REPO, "profiles", OUTNAME.get(name, f"pmc_traffic_{name}.json"))
@@ -80,7 +83,8 @@ for name, (K, W, kern, short, spl, simds) in LINES.items():
                        f"({name}); 2 cycles per wave VALU issue, 2.4 GHz; per-dispatch sums in "
                        f"{os.path.relpath(dst_csv, REPO)} (tools/gpu_pmc_all.sh, tools/pmc_fold_r04.py)")
         json.dump(d, open(outj, "w"), indent=1)
-    st = first(f"{D}/{name}_stats/**/*kernel_stats.csv")
-    if st:
-        shutil.copy(st, os.path.join(OUT, f"{name}_kernel_stats.csv"))
+    st = first(f"{D}/{name}_stats/**/*results.db")
+    if st:  # rocprofv3 --kernel-trace --stats of the same line: per-kernel statistics (tools/rocpd_stats.py)
+        subprocess.run([sys.executable, os.path.join(REPO, "tools", "rocpd_stats.py"), st,
+                        os.path.join(OUT, f"{name}_kernel_stats.csv")], check=True, cwd=REPO, stdout=subprocess.DEVNULL)
 print("folded into profiles/pmc_*.json; raw files under profiles/r04/pmc/")
