@@ -188,7 +188,7 @@ struct ResidentLaunch {
   // CUs x workgroups per CU from the occupancy API, cached per device
   template <bool TR>
   static int cap_of() {
-    static int cached_dev = -1, cached_cap = 0;
+    static thread_local int cached_dev = -1, cached_cap = 0;  // per thread: no shared mutable state
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (dev != cached_dev) {
@@ -210,8 +210,8 @@ struct StreamLaunch {
   // one workgroup per co-resident slot (CUs x the occupancy API, cached per device and LDS size), at
   // most one per tile; no workgroup waits for another, so any grid is correct
   static hipError_t launch(const StepParams& p, int R, size_t smem, hipStream_t s) {
-    static int cached_dev = -1, cached_cap = 0;
-    static size_t cached_smem = 0;
+    static thread_local int cached_dev = -1, cached_cap = 0;  // per thread: no shared mutable state
+    static thread_local size_t cached_smem = 0;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
