@@ -797,13 +797,24 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   // Resident launches of different handles (streams) on one device never overlap: two grids that
   // each hold part of the CUs would wait for each other's missing workgroups.
   GridOrderScope order(h->device, h->stream);
-  if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));
+  // timing: the start event is a marker queued right before the launch, the stop event is stamped
+  // by the plain launch's own dispatch (hipExtLaunchKernel): the interval covers the kernel and
+  // nothing queued after it, and the run's wall time stays that of two markers (a dispatch-stamped
+  // start costs ~3 us of host time before the launch; profiles/r04/ab/README.md).  Cooperative
+  // launches keep both markers.  PF_EXT_EVENTS (A/B): 0 markers, 1 both stamped by the dispatch,
+  // 2 start only, 3 stop only (default)
+  const char* xe_env = std::getenv("PF_EXT_EVENTS");
+  const int xe = xe_env ? std::atoi(xe_env) : 3;
+  const bool ext0 = h->timing && !coop && (xe == 1 || xe == 2), ext1 = h->timing && !coop && (xe == 1 || xe == 3);
+  if (h->timing && !ext0) HIPCHK(hipEventRecord(h->tev[0], h->stream));
   for (int r0 = 0; r0 < h->R; r0 += Rg) {
     q.r0 = r0;
     q.arrive = h->rsync + arr_off;
     q.arrive0 = h->res_arrive;
     q.seq = ++h->res_seq;
-    const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream, coop);
+    const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream, coop,
+                                          (ext0 && r0 == 0) ? h->tev[0] : nullptr,
+                                          (ext1 && r0 + Rg >= h->R) ? h->tev[1] : nullptr);
     if (e == hipSuccess) h->res_arrive += (unsigned long long)G * std::min(Rg, h->R - r0);
     if (e == hipErrorCooperativeLaunchTooLarge && r0 == 0) {
       (void)hipGetLastError();
@@ -811,7 +822,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     }
     if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_resident launch: ") + hipGetErrorString(e));
   }
-  if (h->timing) HIPCHK(hipEventRecord(h->tev[1], h->stream));
+  if (h->timing && !ext1) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   order.end();
   h->res_hdr = q.hdr_out;  // the state is now what this run's exit header describes
   h->res_tag += (uint32_t)tag_span;

@@ -3,6 +3,7 @@
 // templates for its model family and registers an Ops entry; pf_engine.hip
 // looks the entry up at pf_create time.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -36,7 +37,8 @@ struct Ops {
   // register-resident whole-run kernel (scalar fp32 models only; null otherwise).
   // Cooperative launch: returns hipErrorCooperativeLaunchTooLarge when the grid
   // cannot be co-resident (the caller then runs the launch-per-step path).
-  hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t, bool coop);
+  // ev0 / ev1 (plain launches; null: none): the launch's own start / stop timestamps
+  hipError_t (*resident)(const ResParams&, int G, int R, hipStream_t, bool coop, hipEvent_t ev0, hipEvent_t ev1);
   // persistent fused step of the many-replicate fp32 scalar launches (pf_step_stream.h; null otherwise):
   // grid = min(G R, co-resident workgroups), tiles walked with the next tile's operands in flight
   hipError_t (*stream)(const StepParams&, int R, size_t smem, hipStream_t);
@@ -172,18 +174,16 @@ struct ResidentLaunch {
   // kernel verifies co-residency itself either way (res_arrive / res_try_abort).
   // hipErrorCooperativeLaunchTooLarge -> the caller runs the launch-per-step path.
   // p.tr_x set: the trace instance (the same kernel plus the verification-trace stores; tests)
-  static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s, bool coop) {
+  // ev0 / ev1 (plain launches): timing events stamped by the kernel's own dispatch
+  // (hipExtLaunchKernel), instead of two marker packets queued around it
+  static hipError_t launch(const ResParams& p, int G, int R, hipStream_t s, bool coop, hipEvent_t ev0, hipEvent_t ev1) {
     const bool tr = p.tr_x != nullptr;
     const void* fn = tr ? (const void*)k_resident<float, NX, NZ, TK, OK, true> : (const void*)k_resident<float, NX, NZ, TK, OK>;
-    if (coop) {
-      ResParams q = p;
-      void* args[] = {&q};
-      return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
-    }
+    ResParams q = p;
+    void* args[] = {&q};
+    if (coop) return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
     if ((long long)G * R > (long long)(tr ? cap_of<true>() : cap())) return hipErrorCooperativeLaunchTooLarge;
-    if (tr) hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK, true>), dim3(G, R), dim3(RBS), 0, s, p);
-    else hipLaunchKernelGGL((k_resident<float, NX, NZ, TK, OK>), dim3(G, R), dim3(RBS), 0, s, p);
-    return hipGetLastError();
+    return hipExtLaunchKernel(fn, dim3(G, R), dim3(RBS), args, 0, s, ev0, ev1, 0);
   }
   // CUs x workgroups per CU from the occupancy API, cached per device
   template <bool TR>

@@ -4,6 +4,10 @@
 // Two such grids issued on different streams (two handles) could each hold part of the CUs
 // and wait for their missing workgroups forever.  A launch on another stream than the previous
 // one therefore waits, on the device, for that one to finish (hipStreamWaitEvent: no host sync).
+// The event is recorded lazily: only when a grid comes on another stream, on the previous stream
+// at that moment (it then covers everything issued there so far, that grid included - a wait
+// that can only be longer than needed, never shorter).  Runs that stay on one stream queue no
+// marker at all (one marker packet cost ~5 us of wall time per resident run, profiles/r04/ab).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -39,13 +43,16 @@ class GridOrderScope {
     if (dev < 0 || dev >= 64 || grid_order_off()) return;
     lk_ = std::unique_lock<std::mutex>(grid_order().mu);
     GridOrder& o = grid_order();
-    if (o.ev[dev] && o.last[dev] && o.last[dev] != s) (void)hipStreamWaitEvent(s, o.ev[dev], 0);
+    if (o.last[dev] && o.last[dev] != s) {
+      if (!o.ev[dev] && hipEventCreateWithFlags(&o.ev[dev], hipEventDisableTiming) != hipSuccess) o.ev[dev] = nullptr;
+      // no event: nothing to order by but the host (rare: event creation failed)
+      if (!o.ev[dev] || hipEventRecord(o.ev[dev], o.last[dev]) != hipSuccess || hipStreamWaitEvent(s, o.ev[dev], 0) != hipSuccess)
+        (void)hipStreamSynchronize(o.last[dev]);
+    }
   }
   void end() {
     if (!lk_.owns_lock()) return;
-    GridOrder& o = grid_order();
-    if (!o.ev[dev_] && hipEventCreateWithFlags(&o.ev[dev_], hipEventDisableTiming) != hipSuccess) o.ev[dev_] = nullptr;
-    if (o.ev[dev_] && hipEventRecord(o.ev[dev_], s_) == hipSuccess) o.last[dev_] = s_;
+    grid_order().last[dev_] = s_;
     lk_.unlock();
   }
   ~GridOrderScope() { end(); }

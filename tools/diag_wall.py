@@ -2,7 +2,7 @@
 pf_run_device launch.  Prints per-variant wall us per 20-step run (median of many runs)
 next to the device time of the same runs (pf_last_run_ms).
 
-    python tools/diag_wall.py
+    python tools/diag_wall.py          (PF_NO_ORDER=1: without the grid-order event)
 """
 import os
 import sys
@@ -66,10 +66,15 @@ def main():
         print(f"{label:34s} wall {np.median(walls):7.1f} us  host call {np.median(launch):6.1f} us  "
               f"device {np.median(devs) if devs else float('nan'):7.1f} us", flush=True)
 
-    measure("timing on, torch sync", True, torch.cuda.synchronize)
-    measure("timing off, torch sync", False, torch.cuda.synchronize)
-    measure("timing off, pf_synchronize", False, lambda: lib.pf_synchronize(pf.handle))
-    measure("timing on, torch sync (again)", True, torch.cuda.synchronize)
+    tag = " [PF_NO_ORDER=1]" if os.environ.get("PF_NO_ORDER") == "1" else ""
+    modes = {"0": "markers", "1": "dispatch events", "2": "dispatch start, marker stop", "3": "marker start, dispatch stop"}
+    for rnd in range(2):
+        for m, name in modes.items():
+            os.environ["PF_EXT_EVENTS"] = m
+            measure(f"timing on ({name}){tag}", True, torch.cuda.synchronize)
+        measure(f"timing off, torch sync{tag}", False, torch.cuda.synchronize)
+    os.environ["PF_EXT_EVENTS"] = "1"
+    measure(f"timing off, pf_synchronize{tag}", False, lambda: lib.pf_synchronize(pf.handle))
     pf.close()
 
 
