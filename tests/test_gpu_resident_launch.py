@@ -12,7 +12,8 @@ one workgroup more than the grid has, i.e. forces that abort.
 * pf_run_device reports the abort at pf_synchronize (PFRetry) with the state unchanged; the
   next run (now cooperative) continues as if the aborted one never happened;
 * two handles' resident runs issued back to back on their own streams are serialised on the
-  device (two partial grids would wait for each other) and equal their one-at-a-time results.
+  device (two partial grids would wait for each other) and equal their one-at-a-time results,
+  also when both grids fill the device and their launches alternate.
 """
 
 import ctypes as C
@@ -175,6 +176,50 @@ def test_two_handles_back_to_back(data):
         means, neff, flags, _ = run.result()
         assert np.array_equal(means[:, 0], ref.means[:, 0, 0])
         assert np.array_equal(neff[:, 0], ref.neff[:, 0])
+    for pf in pfs:
+        pf.close()
+
+
+def test_two_full_grids_interleaved(data):
+    """Two handles whose grids each fill the device (N = 1e6: 245 workgroups, one per CU), their
+    20-step device runs enqueued alternately (A, B, A, B) before any wait.  Each launch that
+    follows the other stream's grid waits for it on the device through the grid-order event, which
+    is recorded lazily on the previous stream at the switch (pf_order.h); two partially resident
+    grids would wait for each other until the co-residency check aborts them (PFRetry).  Both runs
+    equal their one-at-a-time results bitwise."""
+    x0, Z = data
+    Z = Z[:40]
+
+    def mk(seed):
+        return ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]],
+                                   Np=1_000_000, seed=seed)
+
+    lib = NV.load()
+    refs = {}
+    for s in (42, 43):
+        pf = mk(s)
+        pf.initialize([x0], [[0.5]])
+        run = DeviceRun(pf, Z)
+        for lo, hi in ((0, 20), (20, 40)):
+            run.launch(lo, hi)
+            run.sync()
+        assert lib.pf_last_run_resident(pf.handle)
+        refs[s] = run.result()
+        pf.close()
+    pfs = [mk(s) for s in (42, 43)]
+    runs = []
+    for pf in pfs:
+        pf.initialize([x0], [[0.5]])
+        runs.append(DeviceRun(pf, Z))
+    for lo, hi in ((0, 20), (20, 40)):
+        for run in runs:
+            run.launch(lo, hi)
+    for run in runs:
+        run.sync()
+    for run, s in zip(runs, (42, 43)):
+        for a, b in zip(run.result(), refs[s]):
+            assert np.array_equal(a, b)
+    assert refs[42][2].any(), "want resample steps in the window"
     for pf in pfs:
         pf.close()
 
