@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(SB) k_edh_setup(FlowParams p, double* table) {
     __syncthreads();
     double S_ld;
     int S_sg;
-    block_gauss_jordan(aug, NZ, sm + SM::FAC, &S_ld, &S_sg);
+    block_gauss_jordan<NZ>(aug, sm + SM::FAC, &S_ld, &S_sg);
     for (int q = t; q < NX * NZ; q += SB) {  // Gm = -1/2 K S^{-1}  (A = Gm H, edh.py:254)
       const int d = q / NZ, l = q - d * NZ;
       double acc = 0.0;

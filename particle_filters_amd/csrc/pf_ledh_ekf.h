@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(EB) k_ekf_seq(const double* __restrict__ Pm, c
     __syncthreads();
     double ld;
     int sg;
-    block_gauss_jordan(aug, NZ, sm + SM::FAC, &ld, &sg);
+    block_gauss_jordan<NZ>(aug, sm + SM::FAC, &ld, &sg);
     for (int q = t; q < NX * NZ; q += EB) {  // K = (P H^T) S^{-1}
       const int d = q / NZ, c = q - d * NZ;
       double acc = 0.0;

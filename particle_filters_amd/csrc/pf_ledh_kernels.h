@@ -257,24 +257,31 @@ __device__ __forceinline__ double quad_form(const double* d, const double* __res
 // ---------------------------------------------------------------------------
 // block-level small dense algebra in LDS (row-major, no pivoting: S, S - c M are SPD)
 // ---------------------------------------------------------------------------
-// Gauss-Jordan on aug [n][2n] = [S | I] -> [I | S^{-1}]; returns log|det S| and its sign.
-__device__ __forceinline__ void block_gauss_jordan(double* aug, int n, double* fac, double* logabs, int* sign) {
+// Gauss-Jordan on aug [N][2N] = [S | I] -> [I | S^{-1}]; returns log|det S| and its sign.
+// Eliminations run column per lane over all N rows (rows unrolled): each lane's loads of its column
+// are independent of its stores, so they issue together instead of one LDS round trip per element
+// (a flattened row x column loop with a runtime stride serialised them).  Every element gets the
+// same expression as before, a - f * b with the row's factor and the pivot row's entry.
+template <int N>
+__device__ __forceinline__ void block_gauss_jordan(double* aug, double* fac, double* logabs, int* sign) {
   const int t = threadIdx.x, nt = blockDim.x;
-  const int w = 2 * n;
+  constexpr int w = 2 * N;
   double la = 0.0;
   int sg = 1;
-  for (int p = 0; p < n; ++p) {
+  for (int p = 0; p < N; ++p) {
     const double piv = aug[p * w + p];
     la += log(fabs(piv));
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
-    for (int r = t; r < n; r += nt) fac[r] = aug[r * w + p];
+    for (int r = t; r < N; r += nt) fac[r] = aug[r * w + p];
     __syncthreads();
     for (int c = t; c < w; c += nt) aug[p * w + c] = aug[p * w + c] / piv;
     __syncthreads();
-    for (int q = t; q < n * w; q += nt) {
-      const int r = q / w, c = q - r * w;
-      if (r != p) aug[q] = aug[q] - fac[r] * aug[p * w + c];
+    for (int c = t; c < w; c += nt) {
+      const double bp = aug[p * w + c];
+#pragma unroll
+      for (int r = 0; r < N; ++r)
+        if (r != p) aug[r * w + c] = aug[r * w + c] - fac[r] * bp;
     }
     __syncthreads();
   }
@@ -282,22 +289,25 @@ __device__ __forceinline__ void block_gauss_jordan(double* aug, int n, double* f
   *sign = sg;
 }
 
-// LU elimination (no pivoting) of T [n][n] in place; log|det| and sign.
-__device__ __forceinline__ void block_logdet(double* T, int n, double* fac, double* logabs, int* sign) {
+// LU elimination (no pivoting) of T [N][N] in place; log|det| and sign.  Trailing updates column
+// per lane over the rows below the pivot (unrolled, predicated), as in block_gauss_jordan.
+template <int N>
+__device__ __forceinline__ void block_logdet(double* T, double* fac, double* logabs, int* sign) {
   const int t = threadIdx.x, nt = blockDim.x;
   double la = 0.0;
   int sg = 1;
-  for (int p = 0; p < n; ++p) {
-    const double piv = T[p * n + p];
+  for (int p = 0; p < N; ++p) {
+    const double piv = T[p * N + p];
     la += log(fabs(piv));
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
-    for (int r = p + 1 + t; r < n; r += nt) fac[r] = T[r * n + p] / piv;
+    for (int r = p + 1 + t; r < N; r += nt) fac[r] = T[r * N + p] / piv;
     __syncthreads();
-    const int m = n - p - 1;
-    for (int q = t; q < m * m; q += nt) {
-      const int r = p + 1 + q / m, c = p + 1 + q % m;
-      T[r * n + c] = T[r * n + c] - fac[r] * T[p * n + c];
+    for (int c = p + 1 + t; c < N; c += nt) {
+      const double bp = T[p * N + c];
+#pragma unroll
+      for (int r = 0; r < N; ++r)
+        if (r > p) T[r * N + c] = T[r * N + c] - fac[r] * bp;
     }
     __syncthreads();
   }
@@ -317,13 +327,13 @@ __device__ __forceinline__ double flow_logdet(const double* M, const double* R, 
   __syncthreads();
   double ld;
   int sg;
-  block_logdet(T, NZ, fac, &ld, &sg);
+  block_logdet<NZ>(T, fac, &ld, &sg);
   if (sg * S_sg > 0) return ld - S_ld;
   const double eps = 1e-12;
   const double c2 = lam - dlam / (2.0 * (1.0 + eps));
   for (int q = t; q < NZ * NZ; q += nt) T[q] = c2 * M[q] + R[q];
   __syncthreads();
-  block_logdet(T, NZ, fac, &ld, &sg);
+  block_logdet<NZ>(T, fac, &ld, &sg);
   return (double)NX * log1p(eps) + ld - S_ld;
 }
 
@@ -410,7 +420,7 @@ __global__ void __launch_bounds__(SB) k_setup(FlowParams p, double* table) {
   __syncthreads();
   double S_ld;
   int S_sg;
-  block_gauss_jordan(sm + SM::AUG, NZ, sm + SM::FAC, &S_ld, &S_sg);
+  block_gauss_jordan<NZ>(sm + SM::AUG, sm + SM::FAC, &S_ld, &S_sg);
   const double ld = flow_logdet<NX, NZ>(sm + SM::M, sm + SM::R, lam, p.dlam, S_ld, S_sg, sm + SM::T, sm + SM::FAC);
   // Gm = -1/2 K S^{-1}
   for (int q = t; q < NX * NZ; q += SB) {
@@ -1026,7 +1036,7 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
       __syncthreads();
       double S_ld;
       int S_sg;
-      block_gauss_jordan(aug, NZ, sm + SM::FAC, &S_ld, &S_sg);
+      block_gauss_jordan<NZ>(aug, sm + SM::FAC, &S_ld, &S_sg);
       theta += flow_logdet<NX, NZ>(Mm, sm + SM::R, lam, dlam, S_ld, S_sg, sm + SM::TT, sm + SM::FAC);
       // Gm = -1/2 K S^{-1}
       for (int q = t; q < NX * NZ; q += 64) {
