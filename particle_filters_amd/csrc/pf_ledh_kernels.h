@@ -257,20 +257,39 @@ __device__ __forceinline__ double quad_form(const double* d, const double* __res
 // ---------------------------------------------------------------------------
 // block-level small dense algebra in LDS (row-major, no pivoting: S, S - c M are SPD)
 // ---------------------------------------------------------------------------
+// Sum of log|pivot| in pivot order.  pv null: each log in its pivot step (one wave-wide fp64 log per
+// pivot on the serial chain).  pv (N doubles of LDS scratch, written at pv[p] by lane 0 during the
+// elimination): the N logs at once, one per lane, then the same sequential sum - identical value.
+template <int N>
+__device__ __forceinline__ double pivot_logsum(double* pv) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  for (int r = t; r < N; r += nt) pv[r] = log(fabs(pv[r]));
+  __syncthreads();
+  double la = 0.0;
+#pragma unroll
+  for (int p = 0; p < N; ++p) la += pv[p];
+  return la;
+}
+
 // Gauss-Jordan on aug [N][2N] = [S | I] -> [I | S^{-1}]; returns log|det S| and its sign.
 // Eliminations run column per lane over all N rows (rows unrolled): each lane's loads of its column
 // are independent of its stores, so they issue together instead of one LDS round trip per element
 // (a flattened row x column loop with a runtime stride serialised them).  Every element gets the
 // same expression as before, a - f * b with the row's factor and the pivot row's entry.
 template <int N>
-__device__ __forceinline__ void block_gauss_jordan(double* aug, double* fac, double* logabs, int* sign) {
+__device__ __forceinline__ void block_gauss_jordan(double* aug, double* fac, double* logabs, int* sign,
+                                                   double* pv = nullptr) {
   const int t = threadIdx.x, nt = blockDim.x;
   constexpr int w = 2 * N;
   double la = 0.0;
   int sg = 1;
   for (int p = 0; p < N; ++p) {
     const double piv = aug[p * w + p];
-    la += log(fabs(piv));
+    if (pv) {
+      if (t == 0) pv[p] = piv;
+    } else {
+      la += log(fabs(piv));
+    }
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
     for (int r = t; r < N; r += nt) fac[r] = aug[r * w + p];
@@ -285,20 +304,24 @@ __device__ __forceinline__ void block_gauss_jordan(double* aug, double* fac, dou
     }
     __syncthreads();
   }
-  *logabs = la;
+  *logabs = pv ? pivot_logsum<N>(pv) : la;
   *sign = sg;
 }
 
 // LU elimination (no pivoting) of T [N][N] in place; log|det| and sign.  Trailing updates column
 // per lane over the rows below the pivot (unrolled, predicated), as in block_gauss_jordan.
 template <int N>
-__device__ __forceinline__ void block_logdet(double* T, double* fac, double* logabs, int* sign) {
+__device__ __forceinline__ void block_logdet(double* T, double* fac, double* logabs, int* sign, double* pv = nullptr) {
   const int t = threadIdx.x, nt = blockDim.x;
   double la = 0.0;
   int sg = 1;
   for (int p = 0; p < N; ++p) {
     const double piv = T[p * N + p];
-    la += log(fabs(piv));
+    if (pv) {
+      if (t == 0) pv[p] = piv;
+    } else {
+      la += log(fabs(piv));
+    }
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
     for (int r = p + 1 + t; r < N; r += nt) fac[r] = T[r * N + p] / piv;
@@ -311,7 +334,7 @@ __device__ __forceinline__ void block_logdet(double* T, double* fac, double* log
     }
     __syncthreads();
   }
-  *logabs = la;
+  *logabs = pv ? pivot_logsum<N>(pv) : la;
   *sign = sg;
 }
 
@@ -320,20 +343,20 @@ __device__ __forceinline__ void block_logdet(double* T, double* fac, double* log
 // S_ld/S_sg: log|det S| and sign; M, R: LDS matrices; T, fac scratch.
 template <int NX, int NZ>
 __device__ __forceinline__ double flow_logdet(const double* M, const double* R, double lam, double dlam, double S_ld,
-                                              int S_sg, double* T, double* fac) {
+                                              int S_sg, double* T, double* fac, double* pv = nullptr) {
   const int t = threadIdx.x, nt = blockDim.x;
   const double c1 = lam - 0.5 * dlam;
   for (int q = t; q < NZ * NZ; q += nt) T[q] = c1 * M[q] + R[q];
   __syncthreads();
   double ld;
   int sg;
-  block_logdet<NZ>(T, fac, &ld, &sg);
+  block_logdet<NZ>(T, fac, &ld, &sg, pv);
   if (sg * S_sg > 0) return ld - S_ld;
   const double eps = 1e-12;
   const double c2 = lam - dlam / (2.0 * (1.0 + eps));
   for (int q = t; q < NZ * NZ; q += nt) T[q] = c2 * M[q] + R[q];
   __syncthreads();
-  block_logdet<NZ>(T, fac, &ld, &sg);
+  block_logdet<NZ>(T, fac, &ld, &sg, pv);
   return (double)NX * log1p(eps) + ld - S_ld;
 }
 
@@ -1036,8 +1059,9 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
       __syncthreads();
       double S_ld;
       int S_sg;
-      block_gauss_jordan<NZ>(aug, sm + SM::FAC, &S_ld, &S_sg);
-      theta += flow_logdet<NX, NZ>(Mm, sm + SM::R, lam, dlam, S_ld, S_sg, sm + SM::TT, sm + SM::FAC);
+      // zt (R^{-1}(z - e), consumed by c above) is free until apply_A: the pivots' log scratch
+      block_gauss_jordan<NZ>(aug, sm + SM::FAC, &S_ld, &S_sg, zt);
+      theta += flow_logdet<NX, NZ>(Mm, sm + SM::R, lam, dlam, S_ld, S_sg, sm + SM::TT, sm + SM::FAC, zt);
       // Gm = -1/2 K S^{-1}
       for (int q = t; q < NX * NZ; q += 64) {
         const int d = q / NZ, l = q - d * NZ;
