@@ -294,10 +294,11 @@ __device__ __forceinline__ void block_gauss_jordan(double* aug, double* fac, dou
     if (piv == 0.0) sg = 0;
     for (int r = t; r < N; r += nt) fac[r] = aug[r * w + p];
     __syncthreads();
-    for (int c = t; c < w; c += nt) aug[p * w + c] = aug[p * w + c] / piv;
-    __syncthreads();
+    // the lane that scales column c of the pivot row is the lane that eliminates column c: no
+    // barrier between the two (fac is read-only until the next pivot)
     for (int c = t; c < w; c += nt) {
-      const double bp = aug[p * w + c];
+      const double bp = aug[p * w + c] / piv;
+      aug[p * w + c] = bp;
 #pragma unroll
       for (int r = 0; r < N; ++r)
         if (r != p) aug[r * w + c] = aug[r * w + c] - fac[r] * bp;
