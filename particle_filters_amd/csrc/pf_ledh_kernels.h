@@ -938,13 +938,24 @@ __device__ __forceinline__ void obs_jac_block(const double* eta, double* H, doub
   __syncthreads();
 }
 
+// Columns of the observation Jacobian that are zero by the model's form: the acoustic h depends on
+// the target positions only, so its velocity columns (4c + 2, 4c + 3) are exact zeros.  Dot products
+// over H skip them at compile time: a finite x times 0.0 adds a signed zero to a sum that never is
+// -0.0 here, so the sums are bitwise those of the dense loops.
+template <int OK>
+__device__ __forceinline__ constexpr bool h_zero_col(int e) {
+  return OK == PF_OBS_ACOUSTIC && (e & 2) != 0;
+}
+
 // out = Gm (H v): zt scratch (NZ)
-template <int NX, int NZ>
+template <int NX, int NZ, int OK = -1>
 __device__ __forceinline__ void apply_A(const double* H, const double* Gm, const double* v, double* zt, double* out) {
   const int t = threadIdx.x;
   for (int k = t; k < NZ; k += blockDim.x) {
     double acc = 0.0;
-    for (int e = 0; e < NX; ++e) acc += H[k * NX + e] * v[e];
+#pragma unroll
+    for (int e = 0; e < NX; ++e)
+      if (!h_zero_col<OK>(e)) acc += H[k * NX + e] * v[e];
     zt[k] = acc;
   }
   __syncthreads();
@@ -1023,14 +1034,18 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
       obs_jac_block<NX, NZ, OK>(eta, H, sm + SM::HV, Pm);
       for (int k = t; k < NZ; k += 64) {
         double acc = 0.0;
-        for (int e = 0; e < NX; ++e) acc += H[k * NX + e] * eta[e];
+#pragma unroll
+        for (int e = 0; e < NX; ++e)
+          if (!h_zero_col<OK>(e)) acc += H[k * NX + e] * eta[e];
         sm[SM::ZE + k] = sm[SM::HV + k] - acc;  // e = h(eta) - H eta
       }
       // K = P H^T
       for (int q = t; q < NX * NZ; q += 64) {
         const int d = q / NZ, k = q - d * NZ;
         double acc = 0.0;
-        for (int e = 0; e < NX; ++e) acc += sm[SM::P + d * NX + e] * H[k * NX + e];
+#pragma unroll
+        for (int e = 0; e < NX; ++e)
+          if (!h_zero_col<OK>(e)) acc += sm[SM::P + d * NX + e] * H[k * NX + e];
         K[q] = acc;
       }
       __syncthreads();
@@ -1038,7 +1053,9 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
       for (int q = t; q < NZ * NZ; q += 64) {
         const int k = q / NZ, l = q - k * NZ;
         double acc = 0.0;
-        for (int d = 0; d < NX; ++d) acc += H[k * NX + d] * K[d * NZ + l];
+#pragma unroll
+        for (int d = 0; d < NX; ++d)
+          if (!h_zero_col<OK>(d)) acc += H[k * NX + d] * K[d * NZ + l];
         Mm[q] = acc;
         aug[k * 2 * NZ + l] = lam * acc + sm[SM::R + q];
         aug[k * 2 * NZ + NZ + l] = (k == l) ? 1.0 : 0.0;
@@ -1072,14 +1089,14 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
       }
       __syncthreads();
       // b = (I + 2 lam A)[(I + lam A) c + A eta0]   (ledh.py:165)
-      apply_A<NX, NZ>(H, Gm, eta0, zt, t1);       // t1 = A eta0
-      apply_A<NX, NZ>(H, Gm, cv, zt, t2);         // t2 = A c
+      apply_A<NX, NZ, OK>(H, Gm, eta0, zt, t1);   // t1 = A eta0
+      apply_A<NX, NZ, OK>(H, Gm, cv, zt, t2);     // t2 = A c
       for (int d = t; d < NX; d += 64) t1[d] = (cv[d] + lam * t2[d]) + t1[d];  // w
       __syncthreads();
-      apply_A<NX, NZ>(H, Gm, t1, zt, t2);         // t2 = A w
+      apply_A<NX, NZ, OK>(H, Gm, t1, zt, t2);     // t2 = A w
       for (int d = t; d < NX; d += 64) t1[d] = t1[d] + 2.0 * lam * t2[d];      // b
       __syncthreads();
-      apply_A<NX, NZ>(H, Gm, eta, zt, t2);        // t2 = A eta
+      apply_A<NX, NZ, OK>(H, Gm, eta, zt, t2);    // t2 = A eta
       for (int d = t; d < NX; d += 64) eta[d] = eta[d] + dlam * (t2[d] + t1[d]);  // ledh.py:171
       __syncthreads();
     }
