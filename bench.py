@@ -618,6 +618,45 @@ def rmse_vs_ref(wl, Zall, truth_all, mean0, cov0, W, K, eng_means, eng_flags, pr
             "ref_threads": oracle_threads() if wl.nx == 1 else 1}
 
 
+def paired_free_run(name, device=0, fixture=None):
+    """SURVEY 8(c)(i) for the large-state configs: the engine's native-Philox free runs of
+    oracle/free_run.CONFIGS[name] (R replicates x N particles from initialize, seed 42, replicate
+    ids 0..R-1, fp32) against the fp64 oracle's runs on the same draws (committed numbers,
+    tests/golden/free_run_pairs.npz): per-replicate RMSE / log-likelihood / resample rate (/ OMAT),
+    mean paired difference within 3 standard errors.  Returns (verdict, engine, oracle) where
+    engine / oracle map each statistic to its per-replicate array."""
+    from oracle import free_run as FR
+    from particle_filters_amd.batch import ParticleFilterBatch
+
+    cfg = FR.CONFIGS[name]
+    T, W, nt = cfg["T"], cfg["W"], cfg.get("n_targets")
+    if fixture is None:
+        fixture = np.load(os.path.join(REPO, "tests", "golden", "free_run_pairs.npz"), allow_pickle=False)
+    if list(fixture[f"{name}_config"]) != [cfg["R"], cfg["N"], T, W, cfg["seed"]]:
+        raise ValueError(f"free_run_pairs.npz {name}: configuration differs from oracle/free_run.CONFIGS")
+    wl = WORKLOADS[name]()
+    g, h, Q, R, Z, truth, mean0, cov0 = wl.build(T, 0)
+    pf = ParticleFilterBatch(g, h, Q, R, Np=cfg["N"], n_replicates=cfg["R"], seed=cfg["seed"], device=device)
+    try:
+        pf.initialize(mean0, cov0)
+        res = pf.run(np.asarray(Z[:T], float), with_cov=False)
+    finally:
+        pf.close()
+    truth = np.asarray(truth[:T], float)
+    eng_rows, ora_rows = [], []
+    for r in range(cfg["R"]):
+        eng_rows.append(FR.summarise(FR.per_step(res.means[:, r], res.flags[:, r], res.log_norm[:, r], truth, nt), W))
+        ora = {k: fixture[f"{name}_{k}"][r] for k in ("err2", "flags", "lse", "omat") if f"{name}_{k}" in fixture}
+        ora_rows.append(FR.summarise(ora, W))
+    eng = {k: np.array([s[k] for s in eng_rows]) for k in eng_rows[0]}
+    ora = {k: np.array([s[k] for s in ora_rows]) for k in ora_rows[0]}
+    v = FR.paired_verdict(eng, ora)
+    v.update({"config": dict(cfg), "window": f"steps [{W}, {T}) after initialize",
+              "oracle": "oracle/sir_philox.py PhiloxSIROracle (fp64 NumPy restatement of particle_filter.py) on the "
+                        "engine's Philox draws, tests/golden/free_run_pairs.npz (make_golden_free_run.py)"})
+    return v, eng, ora
+
+
 def spawn_ranks(n):
     """``bench.py --gpus N`` without a launcher: start N rank processes (RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1) before this process
@@ -928,6 +967,18 @@ def main():
                     sd = float(np.std(rmse, ddof=1))
                     ref["mc_sd_rmse_over_replicates"] = sd
                     ref["abs_diff_in_mc_sd"] = ref["abs_diff"] / sd if sd > 0 else None
+                if wl.nx > 1 and args.precision == "fp32" and wl.name in ("l96", "mat"):
+                    # the parity verdict for the large states: paired multi-replicate free runs
+                    try:
+                        pv, _, _ = paired_free_run(wl.name, device=local)
+                        ref["paired_free_run"] = pv
+                        ref["tolerance"] = ("paired free runs: mean per-replicate difference (engine - fp64 oracle, "
+                                            "same Philox draws) of every statistic within 3 standard errors "
+                                            "(SURVEY 8(c)(i))")
+                        ref["parity_ok"] = pv["ok"]
+                    except Exception as e:
+                        ref["paired_free_run"] = {"error": repr(e)}
+                        log("paired free run failed:", repr(e))
                 if cpu is not None and wl.nx == 1 and "ref_particle_steps_per_s" in ref:
                     th = ref["ref_threads"]
                     cpu["c_openmp"] = {"value": ref["ref_particle_steps_per_s"], "unit": "particle-steps/s",

@@ -222,7 +222,8 @@ pf_status pf_last_run_ms(pf_handle* h, float* ms);
  * recomputation inside the launch: the predicted particles and pre-resample log-weights (fp32,
  * any uniform frame), and on a resample step the ancestor index of every output slot (-1
  * elsewhere).  pf_get_trace copies step t (of the last run) of replicate r: x, l, anc [N]
- * (nullable), and resets that step's ancestors to -1. */
+ * (nullable), and resets that step's ancestors to -1; PF_E_ARG when the last run did not execute
+ * as the resident kernel (a launch-per-step run records no trace). */
 pf_status pf_set_trace(pf_handle* h, int64_t T_cap);
 pf_status pf_get_trace(pf_handle* h, int64_t t, int32_t r, float* x, float* l, int32_t* anc);
 /* Geometry of the step launch: tiles per replicate, tile size, dynamic LDS bytes. */

@@ -168,8 +168,9 @@ class SIROracle:
     """Restatement of ``ParticleFilter`` (pf.py:53-287).
 
     Extra instrumentation (not in the reference, read-only): ``last_neff`` is
-    the pre-resample Neff of the last update and ``last_resampled`` whether
-    ``_resample`` fired (pf.py:203-204).
+    the pre-resample Neff of the last update, ``last_resampled`` whether
+    ``_resample`` fired (pf.py:203-204) and ``last_lse`` the update's log
+    normaliser ``m + log sum exp(logw - m)`` (pf.py:261-262).
     """
 
     def __init__(
@@ -202,6 +203,7 @@ class SIROracle:
         self.LR = np.linalg.cholesky(self.R + 1e-12 * np.eye(self.nz))  # pf.py:107
         self.last_neff = float("nan")
         self.last_resampled = False
+        self.last_lse = float("nan")
 
     # pf.py:110-132
     def initialize(self, mean: Array, cov: Array) -> OracleState:
@@ -275,7 +277,9 @@ class SIROracle:
         quad = np.sum(y * y, axis=0)
         logw = np.log(weights + 1e-300) - 0.5 * quad
         m = np.max(logw)
-        w = np.exp(logw - (m + np.log(np.sum(np.exp(logw - m)))))
+        lse = m + np.log(np.sum(np.exp(logw - m)))
+        self.last_lse = float(lse)  # the log-normaliser (marginal-likelihood increment), read-only
+        w = np.exp(logw - lse)
         particles, w = self._resample(particles, w)
         mean = np.average(particles, axis=0, weights=w)
         cov = np.atleast_2d(np.cov(particles.T, aweights=w, bias=True))
@@ -304,6 +308,7 @@ def run_filter(pf: SIROracle, Z: Array, *, first_update_only: bool = False,
     covs = np.zeros((T, pf.nx, pf.nx))
     ess = np.zeros(T)
     neff = np.zeros(T)
+    lse = np.zeros(T)
     flags = np.zeros(T, dtype=bool)
     for t in range(T):
         z = np.atleast_1d(Z[t])
@@ -315,8 +320,9 @@ def run_filter(pf: SIROracle, Z: Array, *, first_update_only: bool = False,
         covs[t] = st.cov
         ess[t] = pf.effective_sample_size()
         neff[t] = pf.last_neff
+        lse[t] = pf.last_lse
         flags[t] = pf.last_resampled
-    return dict(means=means, covs=covs, ess=ess, neff=neff, flags=flags,
+    return dict(means=means, covs=covs, ess=ess, neff=neff, lse=lse, flags=flags,
                 final_particles=pf.state.particles.copy(), final_weights=pf.state.weights.copy(),
                 t_final=pf.state.t)
 

@@ -442,7 +442,7 @@ pf_status launch_step(pf_handle* h, StepParams& p, bool writes_x, bool writes_lw
   // the fused many-replicate fp32 scalar step: the persistent kernel (its paths need the heads, the
   // systematic method, <= 2 chunks of 4 per thread and the state in the record)
   const bool stream = h->stream_mode && h->ops->stream && p.head && p.do_predict && p.do_update == 1 &&
-                      p.method == 0 && h->tile <= 2048 && h->tile >= 512 && h->R <= 1024 && !p.use_lse_ext &&
+                      p.method == 0 && h->tile <= 2048 && h->tile >= STREAM_MIN_TILE && h->R <= 1024 && !p.use_lse_ext &&
                       !p.xr_out && !p.anc_out;
   if (p.do_predict && p.do_update == 1) h->last_stream = stream;
   if (stream) {  // LDS: k_step's gather layout + the replicates' decisions (R ints after the ancestors)
@@ -784,7 +784,9 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   // Replicates are independent filters: when all R do not fit co-resident, groups of as many
   // as fit run one after another (each replicate computes exactly what it computes alone, so
   // the path - and every replicate's result - does not depend on R or on the sharding).
-  const int cap = h->ops->resident_cap ? h->ops->resident_cap() : 0;
+  // with a verification trace set, the trace instance's occupancy sizes the groups (it may fit fewer
+  // workgroups than the plain instance; a group sized for the plain one would not launch resident)
+  const int cap = h->ops->resident_cap ? h->ops->resident_cap(h->tr_x != nullptr) : 0;
   const int Rg = cap >= G ? std::max(1, std::min(h->R, cap / G)) : h->R;
   // Launch mode: one plain launch that checks its own co-residency (ResParams::arrive; ~17 us
   // cheaper than a cooperative launch), or cooperative launches when the run needs several
@@ -1472,6 +1474,8 @@ pf_status pf_get_trace(pf_handle* h, int64_t t, int32_t r, float* x, float* l, i
     const pf_status s0 = settle(h);
     if (s0) return s0;
   }
+  // only the resident kernel records the trace: after a launch-per-step run it would be stale
+  if (!h->last_resident) return fail(PF_E_ARG, "the last run was not a resident launch: no trace recorded");
   HIPCHK(hipStreamSynchronize(h->stream));
   const size_t o = ((size_t)t * h->R + r) * h->Npad, n = (size_t)h->N * 4;
   if (x) HIPCHK(hipMemcpy(x, h->tr_x + o, n, hipMemcpyDeviceToHost));

@@ -941,7 +941,10 @@ __device__ __forceinline__ void obs_jac_block(const double* eta, double* H, doub
 // Columns of the observation Jacobian that are zero by the model's form: the acoustic h depends on
 // the target positions only, so its velocity columns (4c + 2, 4c + 3) are exact zeros.  Dot products
 // over H skip them at compile time: a finite x times 0.0 adds a signed zero to a sum that never is
-// -0.0 here, so the sums are bitwise those of the dense loops.
+// -0.0 here, so the sums are bitwise those of the dense loops.  That equality assumes finite operands:
+// a NaN / Inf in a skipped velocity entry no longer poisons these sums (NaN * 0 would).  A diverged
+// particle still shows up as NaN: the non-finite entry stays in its own flow components (eta += dlam
+// (A eta + b) keeps it), and the transition density of its weight reads every component.
 template <int OK>
 __device__ __forceinline__ constexpr bool h_zero_col(int e) {
   return OK == PF_OBS_ACOUSTIC && (e & 2) != 0;

@@ -42,7 +42,8 @@ struct Ops {
   // persistent fused step of the many-replicate fp32 scalar launches (pf_step_stream.h; null otherwise):
   // grid = min(G R, co-resident workgroups), tiles walked with the next tile's operands in flight
   hipError_t (*stream)(const StepParams&, int R, size_t smem, hipStream_t);
-  int (*resident_cap)();  // workgroups of k_resident co-resident on the current device (0: unknown)
+  int (*resident_cap)(bool trace);  // workgroups of k_resident (the trace instance when trace) co-resident
+                                    // on the current device (0: unknown)
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
                                 double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t, int nx);
@@ -182,7 +183,7 @@ struct ResidentLaunch {
     ResParams q = p;
     void* args[] = {&q};
     if (coop) return hipLaunchCooperativeKernel(fn, dim3(G, R), dim3(RBS), args, 0, s);
-    if ((long long)G * R > (long long)(tr ? cap_of<true>() : cap())) return hipErrorCooperativeLaunchTooLarge;
+    if ((long long)G * R > (long long)cap(tr)) return hipErrorCooperativeLaunchTooLarge;
     return hipExtLaunchKernel(fn, dim3(G, R), dim3(RBS), args, 0, s, ev0, ev1, 0);
   }
   // CUs x workgroups per CU from the occupancy API, cached per device
@@ -202,7 +203,7 @@ struct ResidentLaunch {
     }
     return cached_cap;
   }
-  static int cap() { return cap_of<false>(); }
+  static int cap(bool trace) { return trace ? cap_of<true>() : cap_of<false>(); }
 };
 
 template <int NZ, int TK, int OK>

@@ -128,6 +128,13 @@ __device__ __forceinline__ void stream_finish(const StepParams& p, int r, int b,
 // path, no pipelining).  The passes have disjoint live ranges, so the streaming pass keeps its
 // registers (the gather path's fp64 search state would otherwise be co-allocated with the prefetched
 // operands).  The replicates' decisions are staged in LDS once (flags: R ints after the ancestors).
+// The smallest tile the host launches k_step_stream with (pf_engine.hip launch_step).  The decisions
+// flags[R] start 12 tile bytes past cdf (the fp64 CDF and the int ancestors of one tile), and the
+// record merge's staging occupies cdf bytes [256, MERGE_LDS_BYTES): the two are disjoint only for
+// tiles of at least MERGE_LDS_BYTES / 12 particles.
+constexpr int STREAM_MIN_TILE = 512;
+static_assert(12 * STREAM_MIN_TILE >= MERGE_LDS_BYTES, "k_step_stream: flags would overlap the merge staging");
+
 #ifndef PF_STREAM_WPE
 #define PF_STREAM_WPE 4
 #endif

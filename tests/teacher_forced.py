@@ -25,9 +25,10 @@ eps_w is the fp32 rounding bound of the engine's log-weights, weighted by the or
 computed per particle from the ORACLE's quantities only (never from a measured engine-oracle
 difference): rnd (1 + |log w0| + |log-likelihood| + sum_j |(R^-1 (z - h))_j| (|h_j| + |z_j|)) - rnd = 8
 unit roundoffs (2^-21 for fp32) over the carried log-weight's shift, the likelihood's operations and
-the fp32 observation / predictions it is built from - plus |ll(x_e) - ll(x_o)|, the oracle's own
-likelihood moved by the predicted particle's rounding (which part 1 bounds separately).  The weights'
-total variation must stay within max(tol_tv, eps_w), Neff within max(tol_neff, 4 eps_w).
+the fp32 observation / predictions it is built from - plus the change of the oracle's likelihood
+under any particle perturbation within part 1's tolerance, tol_x x scale x |J_h^T R^-1 (z - h)|_1
+(the oracle's likelihood gradient, ``ll_rounding_bound``).  The weights' total variation must stay
+within max(tol_tv, eps_w), Neff within max(tol_neff, 4 eps_w).
 """
 
 from __future__ import annotations
@@ -64,9 +65,29 @@ def margins(w, U, idx):
     return np.minimum(pos - lo, cdf[idx] - pos), cdf, pos
 
 
+def ll_rounding_bound(h_vec, X, gz, dx):
+    """Per particle, a bound on |ll(x + d) - ll(x)| over every perturbation |d_k| <= dx (the particle
+    tolerance part 1 checks), from the ORACLE's particles only: ll = 1/2 |LR^-1 (z - h(x))|^2 has the
+    gradient -J_h(x)^T R^-1 (z - h(x)) = -J_h^T gz, so |dll| <= dx |J_h^T gz|_1 to first order; the
+    gradient by central differences of phi(x) = gz . h(x) (gz held fixed), and a factor 1.25 for
+    the second-order term (dx is a few fp32 ulps of the state)."""
+    X = np.asarray(X, float)
+    N, nx = X.shape
+    g1 = np.zeros(N)
+    for k in range(nx):
+        d = 1e-6 * np.maximum(1.0, np.abs(X[:, k]))
+        xp, xm = X.copy(), X.copy()
+        xp[:, k] += d
+        xm[:, k] -= d
+        hp = np.asarray(h_vec(xp), float).reshape(N, -1)
+        hm = np.asarray(h_vec(xm), float).reshape(N, -1)
+        g1 += np.abs(np.sum((hp - hm).T * gz, axis=0) / (2.0 * d))
+    return 1.25 * dx * g1
+
+
 def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_pre, we_pre, neff_e, neff_e0,
              flag_e, mean_e, xe_post, scale, bm24=True, rnd=2.0 ** -21, exp_err=2.0 ** -22, K=8, cov_e=None,
-             cov_floor=1e-6):
+             cov_floor=1e-6, tol_x=2e-6):
     """Compare one engine step with the oracle's from the same state.  Returns a dict of measured
     quantities (see module docstring); tolerances are applied by ``check``."""
     N, nx = x0.shape
@@ -92,8 +113,7 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     # the fp32 rounding bound of the engine's log-weights (module docstring), oracle quantities only
     gz = np.linalg.solve(o.LR.T, resid)  # R^-1 (z - h), [nz][N]
     hz = np.sum(np.abs(gz) * (np.abs(hx.T) + np.abs(zz)[:, None]), axis=0)
-    re = np.linalg.solve(o.LR, (zz - np.asarray(ssm.h_vec(np.asarray(xe_pre, float)), float).reshape(N, -1)).T)
-    dll = np.abs(0.5 * np.sum(re * re, axis=0) - ll)
+    dll = ll_rounding_bound(ssm.h_vec, o.pre_x, gz, tol_x * scale)
     with np.errstate(divide="ignore"):
         lw0 = np.abs(np.log(np.asarray(w0, float) + 1e-300))
     out["eps_w"] = float(np.sum(o.pre_w * (rnd * (1.0 + lw0 + ll + hz) + dll)))

@@ -14,7 +14,8 @@ Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the 
                             fp32 rounding bound of the engine's log-weights, a formula of the
                             oracle's own quantities (tests/teacher_forced.py docstring: 2^-21 (1 +
                             |log w0| + |log-lik| + the observation / prediction terms) + the
-                            likelihood's change under the particles' rounding) - never a measured
+                            oracle likelihood's change under any particle perturbation within the
+                            2e-6 x scale tolerance above, by its gradient) - never a measured
                             engine-vs-oracle difference (MAT's 25 sensors at R = 0.01 I give
                             log-likelihoods of O(1e2-1e4): eps_w grows with them)
   Neff                      rel <= max(1e-5, 4 eps_w)
@@ -105,7 +106,8 @@ def chain(name, T, n_bound=20, reps=None, precision="fp32", expect_resident=None
             c = TF.one_step(ssm, Q, R, seed=42, rep=k, epoch=rs["epoch"], thresh=0.5, method="systematic", reg=False,
                             x0=x0[k], w0=w0[k], z=Z[t], xe_pre=xe_pre[k], we_pre=we_pre[k], neff_e=r.neff[0, k],
                             neff_e0=r0.neff[0, k], flag_e=r.flags[0, k], mean_e=r.means[0, k], xe_post=xe_post[k],
-                            scale=scale, bm24=bm24, cov_e=r.covs[0, k], **(step_kw or {}))
+                            scale=scale, bm24=bm24, cov_e=r.covs[0, k], tol_x=(tol or {}).get("tol_x", 2e-6),
+                            **(step_kw or {}))
             print(f"{name} rep {k}: " + TF.fmt(t, c))
             b = TF.bounds(c, scale=scale, **{k2: v for k2, v in (tol or {}).items() if k2 != "tol_cov"})
             results.append(dict(c, t=int(t), rep=int(k), scale=scale, bound=b,
