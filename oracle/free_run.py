@@ -41,7 +41,7 @@ from .sir_philox import PhiloxSIROracle
 # for config 4: the scored window is the bench's timed window [W, W + K))
 CONFIGS = {
     "l96": dict(R=32, N=100_000, T=100, W=0, seed=42),
-    "mat": dict(R=64, N=100_000, T=110, W=10, seed=42, n_targets=4),
+    "mat": dict(R=128, N=100_000, T=110, W=10, seed=42, n_targets=4),
 }
 STATS = ("rmse", "loglik", "resample_rate", "omat")
 

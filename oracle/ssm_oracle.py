@@ -48,6 +48,9 @@ class SSM:
     h: Callable          # per particle: h(x (nx,)) -> (nz,)
     g_vec: Callable      # vectorised:   g(X (N,nx), u) -> (N,nx)
     h_vec: Callable      # vectorised:   h(X (N,nx)) -> (N,nz)
+    # optional: J_h(x_i)^T g_i per particle, (X (N,nx), G (N,nz)) -> (N,nx) (test bounds; the
+    # analytic Jacobians of the models' h, checked against finite differences by the CPU tests)
+    hjt_vec: Optional[Callable] = None
 
 
 def sv_harness(alpha: float, sigma: float, beta: float, R: float = 0.1) -> SSM:
@@ -76,7 +79,7 @@ def sv_logsq(alpha: float, sigma: float, beta: float) -> SSM:
         return log_beta_sq + x + LOGCHI2_MEAN
 
     return SSM(1, 1, np.array([[sigma ** 2]]), np.array([[LOGCHI2_VAR]]), g, h,
-               lambda X, u: alpha * X, lambda X: log_beta_sq + X + LOGCHI2_MEAN)
+               lambda X, u: alpha * X, lambda X: log_beta_sq + X + LOGCHI2_MEAN, lambda X, G: np.array(G, float))
 
 
 def l96_rhs(x, F):
@@ -93,6 +96,12 @@ def l96_rk4(x, dt, F):
     return x + (dt / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
+def _scatter_cols(X, G, idx):
+    out = np.zeros(np.shape(X))
+    out[:, idx] = G
+    return out
+
+
 def lorenz96(nx: int = 40, F: float = 8.0, dt: float = 0.01, obs_fraction: int = 4,
              obs_error_std: float = 1.0, q_std: float = 0.1) -> SSM:
     """L96 SIR wiring: g = one RK4 step, h = x[H_idx], R = std^2 I, Q = q_std^2 I (build's choice)."""
@@ -100,7 +109,7 @@ def lorenz96(nx: int = 40, F: float = 8.0, dt: float = 0.01, obs_fraction: int =
     nz = H_idx.size
     return SSM(nx, nz, (q_std ** 2) * np.eye(nx), (obs_error_std ** 2) * np.eye(nz),
                lambda x, u: l96_rk4(x, dt, F), lambda x: x[H_idx],
-               lambda X, u: l96_rk4(X, dt, F), lambda X: X[:, H_idx])
+               lambda X, u: l96_rk4(X, dt, F), lambda X: X[:, H_idx], lambda X, G: _scatter_cols(X, G, H_idx))
 
 
 def mat_joint(sensors: np.ndarray, psi: float = 10.0, d0: float = 0.1, n_targets: int = 4,
@@ -150,7 +159,17 @@ def mat_joint(sensors: np.ndarray, psi: float = 10.0, d0: float = 0.1, n_targets
             z += psi / ((dx ** 2 + dy ** 2) + d0)
         return z
 
-    return SSM(nx, ns, Q, R, g, h, g_vec, h_vec)
+    def hjt_vec(X, G):  # d h_s / d p_c = -2 psi (p_c - s) / (|p_c - s|^2 + d0)^2
+        out = np.zeros(X.shape)
+        for c in range(C):
+            dx = X[:, 4 * c, None] - S[None, :, 0]
+            dy = X[:, 4 * c + 1, None] - S[None, :, 1]
+            k = -2.0 * psi / ((dx ** 2 + dy ** 2) + d0) ** 2 * G
+            out[:, 4 * c] = np.sum(k * dx, axis=1)
+            out[:, 4 * c + 1] = np.sum(k * dy, axis=1)
+        return out
+
+    return SSM(nx, ns, Q, R, g, h, g_vec, h_vec, hjt_vec)
 
 
 def linear(A: np.ndarray, H: np.ndarray, Q: np.ndarray, R: np.ndarray) -> SSM:

@@ -65,6 +65,12 @@ __device__ __forceinline__ double lane63_d(double v) {
   const int lo = __builtin_amdgcn_readlane((int)x, 63), hi = __builtin_amdgcn_readlane((int)(x >> 32), 63);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+// lane L's value (L uniform) in every lane
+__device__ __forceinline__ double readlane_d(double v, int L) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, L), hi = __builtin_amdgcn_readlane((int)(x >> 32), L);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 // whole-wave results (uniform: scalar registers)
 __device__ __forceinline__ float wave_max_u(float v) {
   v = row_max_f(v);

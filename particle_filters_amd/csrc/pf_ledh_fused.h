@@ -245,8 +245,8 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   __shared__ double boff[FMAX + 1];   // exclusive prefix of the scaled workgroup sums (+ total)
   __shared__ double xs[FCH * XW];     // raw rows of a chunk (the first flow round's stay from P1)
   __shared__ double ws[FCH];
+  __shared__ double shs[NX];            // P4's moment shift (the previous posterior mean)
   __shared__ int64_t shi[FPPB];       // resample: end of each particle's slot range
-  __shared__ double mred[MB::SL][MB::NPAIR][16];
   __shared__ double pms[L::SIZE];     // the parameter block (the parts the flow reads)
   __shared__ double afs[TL::AFF_SIZE];  // the composed flow
   __shared__ double zs[NZ];             // the step's observation
@@ -385,89 +385,114 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       }
     }
   }
-  m = dpp_reduce_max(m, red);
+  (void)m;
+  __syncthreads();  // every slot's log weight is in lws
+  LF_STAMP(12);
 
   // ---- P2: exponentials relative to the WORKGROUP max, sums and scan (no grid max needed:
   //      the workgroups' (max, sum, sum of squares) combine exactly after one barrier) ----------
-  // thread t owns the contiguous run [t*per, t*per + per) of this workgroup's particles
-  const int per = (n + FB - 1) / FB;
-  double s1 = 0.0, s2 = 0.0;
-  for (int j = t * per; j < min(n, t * per + per); ++j) {
-    const double l = lws[j];
-    const double e = (l > -INFINITY) ? exp(l - m) : 0.0;
-    lws[j] = e;
-    s1 += e;
-    s2 += e * e;
-  }
-  {
-    const double inc = wave_incl_scan_dpp(s1);
-    if (lane == 63) red[wv] = inc;
-    __syncthreads();
-    double off = 0.0;
-    for (int k = 0; k < wv; ++k) off += red[k];
-    double run = off + inc - s1;
-    for (int j = t * per; j < min(n, t * per + per); ++j) {
-      run += lws[j];
-      scan[j] = run;
+  // One wave does it (lane l: particles PL l .. PL l + PL - 1, at most FPPB of them), so that the
+  // workgroup's max, sums and scan cost no barrier beyond the grid barrier's own; the other waves
+  // go straight on to it.
+  if (wv == 0) {
+    constexpr int PL = FPPB / 64;
+    double e[PL], s1 = 0.0, s2 = 0.0, ml = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int j = PL * lane + k;
+      e[k] = j < n ? lws[j] : -INFINITY;
+      ml = fmax(ml, e[k]);
     }
-    __syncthreads();
+    const double mw = wave_max_ud(ml);
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      e[k] = (e[k] > -INFINITY) ? exp(e[k] - mw) : 0.0;
+      s1 += e[k];
+      s2 += e[k] * e[k];
+    }
+    const double inc = wave_incl_scan_dpp(s1);
+    double run = inc - s1, last = 0.0;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int j = PL * lane + k;
+      run += e[k];
+      if (j < n) {
+        lws[j] = e[k];
+        scan[j] = run;
+      }
+      if (j == n - 1) last = run;
+    }
+    const double S_b = lane63_d(inc);
+    const double S2_b = wave_sum_ud(s2);
+    last = readlane_d(last, (n - 1) / PL);  // scan[n - 1], the value this workgroup's slice ends on
+    if (lane == 0) {
+      f_st(p.part + 0 * FMAX + b, mw);
+      f_st(p.part + 1 * FMAX + b, S_b);
+      f_st(p.part + 2 * FMAX + b, S2_b);
+      f_st(p.part + 3 * FMAX + b, last);
+    }
   }
-  const double S_b = dpp_reduce_sum(s1, red);
-  const double S2_b = dpp_reduce_sum(s2, red);
-  if (t == 0) {
-    f_st(p.part + 0 * FMAX + b, m);
-    f_st(p.part + 1 * FMAX + b, S_b);
-    f_st(p.part + 2 * FMAX + b, S2_b);
-    f_st(p.part + 3 * FMAX + b, scan[n - 1]);
-  }
+  LF_STAMP(13);
   LF_STAMP(2);
   if (!f_barrier(p, ph + 1)) return;
   LF_STAMP(3);
 
   // ---- P3: global normaliser, ESS, decision; this slice of the CDF; the ancestors -----------
   // P4's moment shift is loaded here with the partials: one round trip for both
-  const int pair = t % MB::NPAIR, sl = t / MB::NPAIR;
-  int bi = 0, bj = 0;
-  {
-    int rem = pair;
-    while (rem >= MB::NB - bi) { rem -= MB::NB - bi; ++bi; }
-    bj = bi + rem;
-  }
-  double shb_i[4], shb_j[4];  // the shift of this thread's two 4-blocks (written by P5' of other
-                              // workgroups this launch: write-through loads after B1)
+  // P4's moment shift (the previous posterior mean, written by P5' of other workgroups this launch:
+  // write-through loads after B1) staged in LDS with the combine's results
+  if (t < NX) shs[t] = f_ldd(p.shift + t);
+  // the NBK partials combined by one wave (lane l: workgroups KL l .. KL l + KL - 1) in one fixed
+  // order, so every workgroup derives the same normaliser, ESS, decision and CDF slices; one
+  // barrier hands the results to the other waves
+  LF_STAMP(14);
+  if (wv == 0) {
+    constexpr int KL = FMAX / 64;
+    double mk[KL], sk[KL], s2k[KL], slk[KL];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    shb_i[k] = 4 * bi + k < NX ? f_ldd(p.shift + 4 * bi + k) : 0.0;
-    shb_j[k] = 4 * bj + k < NX ? f_ldd(p.shift + 4 * bj + k) : 0.0;
+    for (int k = 0; k < KL; ++k) {
+      const int kk = KL * lane + k;
+      const bool ok = kk < p.nbk;
+      mk[k] = ok ? f_ld(p.part + 0 * FMAX + kk) : -INFINITY;
+      sk[k] = ok ? f_ld(p.part + 1 * FMAX + kk) : 0.0;
+      s2k[k] = ok ? f_ld(p.part + 2 * FMAX + kk) : 0.0;
+      slk[k] = ok ? f_ld(p.part + 3 * FMAX + kk) : 0.0;
+    }
+    double ml = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) ml = fmax(ml, sk[k] > 0.0 ? mk[k] : -INFINITY);
+    const double M = wave_max_ud(ml);
+    double fk[KL], v[KL], sl = 0.0, e2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+      fk[k] = (sk[k] > 0.0) ? exp(mk[k] - M) : 0.0;
+      v[k] = sk[k] * fk[k];
+      sl += v[k];
+      e2 += s2k[k] * fk[k] * fk[k];
+    }
+    const double inc = wave_incl_scan_dpp(sl);
+    const double S = lane63_d(inc);
+    const double E2 = wave_sum_ud(e2);
+    double run = inc - sl;  // exclusive prefix of the scaled workgroup sums
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+      const int kk = KL * lane + k;
+      if (kk < p.nbk) boff[kk] = run;
+      if (kk == b) red[8] = fk[k];  // this workgroup's scale e^(m_b - M)
+      // the predecessor's last CDF value, as that workgroup evaluates its own slice
+      if (kk + 1 == b) red[9] = (run + fk[k] * slk[k]) / S;
+      run += v[k];
+    }
+    if (lane == 0) {
+      boff[FMAX] = S;  // total
+      red[10] = E2;
+    }
   }
-  double mk = -INFINITY, sk = 0.0, s2k = 0.0, slk = 0.0;
-  if (t < p.nbk) {
-    mk = f_ld(p.part + 0 * FMAX + t);
-    sk = f_ld(p.part + 1 * FMAX + t);
-    s2k = f_ld(p.part + 2 * FMAX + t);
-    slk = f_ld(p.part + 3 * FMAX + t);
-  }
-  const double M = dpp_reduce_max(sk > 0.0 ? mk : -INFINITY, red);
-  const double fk = (sk > 0.0) ? exp(mk - M) : 0.0;
-  {
-    const double v = sk * fk;
-    const double inc = wave_incl_scan_dpp(v);
-    if (lane == 63) red[wv] = inc;
-    __syncthreads();
-    double off = 0.0;
-    for (int k = 0; k < wv; ++k) off += red[k];
-    if (t < p.nbk) boff[t] = off + inc - v;  // exclusive prefix of the scaled workgroup sums
-    if (t == FB - 1) boff[FMAX] = off + inc;  // total
-    __syncthreads();
-    if (t == b) red[8] = fk;  // this workgroup's scale e^(m_b - M)
-    // the predecessor's last CDF value, as that workgroup evaluates its own slice
-    if (t + 1 == b) red[9] = (boff[t] + fk * slk) / boff[FMAX];
-    __syncthreads();
-  }
+  __syncthreads();
   const double S = boff[FMAX];
   const double fb = red[8];
   const double lastprev = b > 0 ? red[9] : -INFINITY;
-  const double E2 = dpp_reduce_sum(s2k * fk * fk, red);
+  const double E2 = red[10];
   const double ess = 1.0 / (E2 / (S * S));
   const bool flag = (p.ratio > 0.0) && (ess < p.ratio * (double)N);
   if (b == 0 && t == 0) {
@@ -477,6 +502,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     if (p.o_ess) *p.o_ess = ess;
     if (p.o_flag) *p.o_flag = flag ? 1 : 0;
   }
+  LF_STAMP(15);
   const double dN = (double)N;
   const double Ob = boff[b];
   int64_t slo0 = 0;
@@ -513,12 +539,28 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
 
   // ---- P4: moment partials of the reported set from the own rows --------------------------
   // after a resample particle j stands for its n_j slots (weight n_j / N): the same sums as over
-  // the post-resample slots; otherwise its normalised weight
-  double a0acc = 0.0, a1[4] = {0.0, 0.0, 0.0, 0.0};  // W (pair 0), S1 of block bi (diagonal pairs)
-  const bool diagp = bi == bj;
-  double acc[16];
+  // the post-resample slots; otherwise its normalised weight.  All of them - W = sum w_j, S1 =
+  // sum w_j u_j and the upper triangle of S2 = sum w_j u_j u_j^T (u_j = row_j - shift) - are the
+  // augmented Gram matrix G = sum_j w_j [u_j; 1][u_j; 1]^T, accumulated on the fp64 matrix cores
+  // (v_mfma_f64_16x16x4: A[d][j] = w_j [u_j; 1]_d, B[j][e] = [u_j; 1]_e, 4 rows per instruction):
+  // 16 x 16 tiles (I, J), I <= J, wave w owning tiles w, w + NW, ...; each lane then stores the
+  // entries of the tiles it holds.  No cross-thread reduction, no LDS staging of partial sums.
+  constexpr int NT = (NX + 1 + 15) / 16;      // tiles per dimension of the augmented Gram matrix
+  constexpr int NPT = NT * (NT + 1) / 2;      // upper-triangular tile pairs
+  constexpr int NW = FB / 64;
+  constexpr int TPW = (NPT + NW - 1) / NW;    // tile pairs per wave (at most)
+  typedef double dbl4 __attribute__((ext_vector_type(4)));
+  dbl4 gacc[TPW];
+  int ti[TPW], tj[TPW];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = 0.0;
+  for (int q = 0; q < TPW; ++q) {
+    gacc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    int rem = wv + q * NW, I = 0;  // pair index -> (I, J), row-major over the upper triangle
+    while (rem >= NT - I && I < NT) { rem -= NT - I; ++I; }
+    ti[q] = I;
+    tj[q] = I + rem;
+  }
+  const int r16 = lane & 15, kq = lane >> 4;  // A row / B column in the tile; k within the 4-row step
   for (int c0 = 0; c0 < n; c0 += FCH) {
     const int cn = min(FCH, n - c0);
     __syncthreads();  // the previous chunk has consumed xs
@@ -541,59 +583,37 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       ws[j] = wj;
     }
     __syncthreads();
-    if (sl < MB::SL) {
-#pragma unroll 4
-      for (int j = sl; j < cn; j += MB::SL) {
-        const double* r = xs + j * XW;
-        const double wj = ws[j];
-        double u[4], v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          u[k] = (r[4 * bi + k] - shb_i[k]) * wj;
-          v[k] = r[4 * bj + k] - shb_j[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int l = 0; l < 4; ++l) acc[k * 4 + l] += u[k] * v[l];
-        if (diagp) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) a1[k] += u[k];
-          if (pair == 0) a0acc += wj;
-        }
+    for (int q = 0; q < TPW; ++q) {
+      if (wv + q * NW >= NPT) break;  // uniform per wave
+      const int da = 16 * ti[q] + r16, db = 16 * tj[q] + r16;
+      const double sa = da < NX ? shs[da] : 0.0, sb = db < NX ? shs[db] : 0.0;
+      for (int j0 = 0; j0 < cn; j0 += 4) {
+        const int j = j0 + kq;
+        const bool live = j < cn;
+        const double wj = live ? ws[j] : 0.0;
+        const double ua = da < NX ? (live ? xs[j * XW + da] - sa : 0.0) : (da == NX ? 1.0 : 0.0);
+        const double ub = db < NX ? (live ? xs[j * XW + db] - sb : 0.0) : (db == NX && live ? 1.0 : 0.0);
+        gacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua * wj, ub, gacc[q], 0, 0, 0);
       }
     }
   }
-  __syncthreads();
+  LF_STAMP(16);
   unsigned long long* cp = p.cpart + (int64_t)b * MM::E;
-  __shared__ double s1red[MB::SL][MB::NB * 4 + 1];
-  if (sl < MB::SL) {
+  // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-    for (int k = 0; k < 16; ++k) mred[sl][pair][k] = acc[k];
-    if (diagp)
+  for (int q = 0; q < TPW; ++q) {
+    if (wv + q * NW >= NPT) break;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s1red[sl][1 + 4 * bi + k] = a1[k];
-    if (pair == 0) s1red[sl][0] = a0acc;
+    for (int r = 0; r < 4; ++r) {
+      const int d = 16 * ti[q] + kq + 4 * r, e = 16 * tj[q] + r16;
+      const double v = gacc[q][r];
+      if (d < NX && e < NX && d <= e) f_st(cp + 1 + NX + (d * NX - d * (d - 1) / 2 + (e - d)), v);
+      else if (d < NX && e == NX) f_st(cp + 1 + d, v);   // S1
+      else if (d == NX && e == NX) f_st(cp, v);          // W
+    }
   }
-  __syncthreads();
-  if (t <= NX) {  // W and S1 over the slices (fixed order)
-    double a = 0.0;
-    for (int s2 = 0; s2 < MB::SL; ++s2) a += s1red[s2][t];
-    f_st(cp + t, a);
-  }
-  if (t < MB::NPAIR) {
-    int ci = 0, rem = t;
-    while (rem >= MB::NB - ci) { rem -= MB::NB - ci; ++ci; }
-    const int cj = ci + rem;
-    for (int k = 0; k < 4; ++k)
-      for (int l = 0; l < 4; ++l) {
-        const int d = 4 * ci + k, e = 4 * cj + l;
-        if (d >= NX || e >= NX || e < d) continue;
-        double a = 0.0;
-        for (int s2 = 0; s2 < MB::SL; ++s2) a += mred[s2][t][k * 4 + l];
-        f_st(cp + 1 + NX + (d * NX - d * (d - 1) / 2 + (e - d)), a);
-      }
-  }
+  LF_STAMP(17);
   LF_STAMP(5);
 }
 

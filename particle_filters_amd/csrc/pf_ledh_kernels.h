@@ -46,9 +46,10 @@ namespace pf {
 namespace ledh {
 
 // diagnostic phase stamps (PF_STAMPS builds only): s_memrealtime (100 MHz) per workgroup, slots
-// 0-5 the fused step's phases (pf_ledh_fused.h), 6-11 the first flow round's sub-phases
+// 0-5 the fused step's phases (pf_ledh_fused.h), 6-11 the first flow round's sub-phases, 12-19 the
+// sub-phases of P2-P4
 #ifdef PF_STAMPS
-constexpr int FST = 12;
+constexpr int FST = 20;
 __device__ unsigned long long g_ledh_stamps[256 * FST];
 #define LF_STAMP(k)                                                                          \
   do {                                                                                       \
@@ -195,7 +196,7 @@ __device__ __forceinline__ void normals_range(uint64_t seed, int64_t f0, uint32_
   for (int gg = 0; gg < GMAX; ++gg) {
     const int64_t g = g0 + gg;
     if (g <= g1) {
-      const Normal4<double> q4 = normal4<double>(seed, (uint32_t)g, 0u, epoch, stream);
+      const Normal4<double> q4 = normal4_bm24d(seed, (uint32_t)g, 0u, epoch, stream);
       // flat index 4g + e lands in slot 4g + e - f0 = 4 gg + e - (f0 & 3)
       const int sh = (int)(f0 & 3);
 #pragma unroll
@@ -220,7 +221,7 @@ __device__ __forceinline__ void noise_thread(const FlowParams& p, int64_t i, dou
 #pragma unroll
     for (int d = 0; d < NX; ++d) {
       const int64_t f = i * NX + d;
-      n[d] = normal4<double>(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS).v[f & 3];
+      n[d] = pick4(normal4_bm24d(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS), (int)(f & 3));
     }
 #pragma unroll
     for (int d = 0; d < NX; ++d) {
@@ -1011,7 +1012,7 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
         vd = p.v_host[i * NX + d];
       } else if (p.noise == PF_NOISE_DEVICE) {
         const int64_t f = i * NX + d;
-        t1[d] = normal4<double>(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS).v[f & 3];
+        t1[d] = pick4(normal4_bm24d(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS), (int)(f & 3));
       }
       sm[SM::V + d] = vd;
     }

@@ -32,12 +32,6 @@ struct StreamPre {  // one tile's operands, loaded one tile ahead
   float z[NZ];                        // the replicate's observation
 };
 
-__device__ __forceinline__ double readlane_d(double v, int q) {
-  const long long x = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)x, q), hi = __builtin_amdgcn_readlane((int)(x >> 32), q);
-  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-
 template <int BS, int NZ>
 __device__ __forceinline__ void stream_fetch(const StepParams& p, int id, StreamPre<NZ>& f) {
   const int t = threadIdx.x;

@@ -117,6 +117,26 @@ __device__ __forceinline__ Normal4<double> normal4<double>(uint64_t seed, uint32
                                        (uint32_t)(seed >> 32)));
 }
 
+// The flow filters' (LEDH / EDH, fp64 state) process-noise normals: the fp32 Box-Muller of the
+// SIR engine's fp32 path (24-bit uniforms, hardware transcendentals) widened to double.  The
+// fp64 Box-Muller (sincospi, log, sqrt in double) cost ~200 fp64 instructions per 4 normals and
+// was the longest phase of the fused LEDH step's per-particle chain; a normal with 24-bit
+// resolution is a draw of the same N(0, 1) (the reference's own draws come from NumPy's PCG64
+// and are not reproduced bit for bit in device-RNG mode anyway).
+__device__ __forceinline__ Normal4<double> normal4_bm24d(uint64_t seed, uint32_t group, uint32_t rep,
+                                                         uint32_t epoch, uint32_t stream) {
+  const Normal4<float> f = normal4<float>(seed, group, rep, epoch, stream);
+  return Normal4<double>{{(double)f.v[0], (double)f.v[1], (double)f.v[2], (double)f.v[3]}};
+}
+
+// element k (0..3, a run-time index) by selects: indexing the register array with k would put
+// it in scratch memory
+template <typename Real>
+__device__ __forceinline__ Real pick4(const Normal4<Real>& q, int k) {
+  const Real lo = (k & 1) ? q.v[1] : q.v[0], hi = (k & 1) ? q.v[3] : q.v[2];
+  return (k & 2) ? hi : lo;
+}
+
 // One [0,1) double per (index, replicate, epoch) on the resample stream.
 __host__ __device__ __forceinline__ double uniform53(uint64_t seed, uint32_t index, uint32_t rep,
                                                      uint32_t epoch) {

@@ -65,14 +65,17 @@ def margins(w, U, idx):
     return np.minimum(pos - lo, cdf[idx] - pos), cdf, pos
 
 
-def ll_rounding_bound(h_vec, X, gz, dx):
+def ll_rounding_bound(h_vec, X, gz, dx, hjt_vec=None):
     """Per particle, a bound on |ll(x + d) - ll(x)| over every perturbation |d_k| <= dx (the particle
     tolerance part 1 checks), from the ORACLE's particles only: ll = 1/2 |LR^-1 (z - h(x))|^2 has the
     gradient -J_h(x)^T R^-1 (z - h(x)) = -J_h^T gz, so |dll| <= dx |J_h^T gz|_1 to first order; the
-    gradient by central differences of phi(x) = gz . h(x) (gz held fixed), and a factor 1.25 for
-    the second-order term (dx is a few fp32 ulps of the state)."""
+    gradient from the model's analytic J_h^T (ssm.hjt_vec) or by central differences of
+    phi(x) = gz . h(x) (gz held fixed), and a factor 1.25 for the second-order term (dx is a few
+    fp32 ulps of the state)."""
     X = np.asarray(X, float)
     N, nx = X.shape
+    if hjt_vec is not None:
+        return 1.25 * dx * np.sum(np.abs(np.asarray(hjt_vec(X, np.asarray(gz, float).T), float)), axis=1)
     g1 = np.zeros(N)
     for k in range(nx):
         d = 1e-6 * np.maximum(1.0, np.abs(X[:, k]))
@@ -113,7 +116,7 @@ def one_step(ssm, Q, R, *, seed, rep, epoch, thresh, method, reg, x0, w0, z, xe_
     # the fp32 rounding bound of the engine's log-weights (module docstring), oracle quantities only
     gz = np.linalg.solve(o.LR.T, resid)  # R^-1 (z - h), [nz][N]
     hz = np.sum(np.abs(gz) * (np.abs(hx.T) + np.abs(zz)[:, None]), axis=0)
-    dll = ll_rounding_bound(ssm.h_vec, o.pre_x, gz, tol_x * scale)
+    dll = ll_rounding_bound(ssm.h_vec, o.pre_x, gz, tol_x * scale, getattr(ssm, "hjt_vec", None))
     with np.errstate(divide="ignore"):
         lw0 = np.abs(np.log(np.asarray(w0, float) + 1e-300))
     out["eps_w"] = float(np.sum(o.pre_w * (rnd * (1.0 + lw0 + ll + hz) + dll)))

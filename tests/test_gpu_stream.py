@@ -65,7 +65,7 @@ def test_stream_equals_tile_grid_models(monkeypatch, obs, control):
     """The other observation kinds the persistent kernel is instantiated for, and a control input.
     (Host-replayed noise / uniforms never reach it: pf_predict with replay normals is a predict-only
     launch, and k_step_stream runs only fused predict + update steps.)"""
-    N, R, T = 6000, 512, 30
+    N, R, T = 6000, 1024, 30  # R x G >= 2048: the per-replicate heads, hence the persistent kernel
     a = _run(monkeypatch, True, N, R, T, obs=obs, control=control)
     b = _run(monkeypatch, False, N, R, T, obs=obs, control=control)
     assert a["streamed"] and not b["streamed"]

@@ -32,10 +32,25 @@ def test_bound_covers_perturbations(make, scale):
     r0 = np.linalg.solve(LR, (z - np.asarray(ssm.h_vec(X), float).reshape(N, -1)).T)
     gz = np.linalg.solve(LR.T, r0)
     dx = 2e-6 * scale
-    b = ll_rounding_bound(ssm.h_vec, X, gz, dx)
+    b = ll_rounding_bound(ssm.h_vec, X, gz, dx, ssm.hjt_vec)
     worst = np.zeros(N)
     for _ in range(8):
         d = rs.choice([-dx, dx], size=X.shape)  # corners of the tolerance box
         worst = np.maximum(worst, np.abs(ll(X + d) - ll(X)))
     assert np.all(worst <= b + 1e-12 * (1 + np.abs(ll(X)))), float(np.max(worst / np.maximum(b, 1e-300)))
     assert np.median(worst / np.maximum(b, 1e-300)) > 0.05  # not vacuous
+
+
+@pytest.mark.parametrize("make,scale", [(lambda: ssm_oracle.sv_logsq(0.95, 0.2, 1.0), 1.0),
+                                        (lambda: ssm_oracle.lorenz96(40), 8.0), (_mat, 40.0)])
+def test_analytic_jacobian_matches_differences(make, scale):
+    """The models' analytic J_h^T g (ssm.hjt_vec, used by the GPU tests) equals the central
+    differences of g . h(x)."""
+    ssm = make()
+    assert ssm.hjt_vec is not None
+    rs = np.random.default_rng(2)
+    X = rs.normal(0.0, 1.0, (500, ssm.nx)) * (scale / 2) + (scale / 2)
+    gz = rs.normal(0.0, 1.0, (ssm.nz, 500))
+    a = ll_rounding_bound(ssm.h_vec, X, gz, 1e-6, ssm.hjt_vec)
+    b = ll_rounding_bound(ssm.h_vec, X, gz, 1e-6)
+    np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-12)
