@@ -84,6 +84,15 @@ struct LL {
     }
   }
   static hipError_t flow_wave(const FlowParams& p, int grid, hipStream_t s) {
+    if constexpr (OK == PF_OBS_ACOUSTIC) {
+      // the acoustic h reads the positions only: the flow's algebra in their NX / 2 dimensions
+      // (k_flow_wave_lr); PF_FLOW_LR=0 runs the observation-space kernel (A/B)
+      static const bool lr = !(std::getenv("PF_FLOW_LR") && std::atoi(std::getenv("PF_FLOW_LR")) == 0);
+      if (lr && p.r_diag) {  // U = R^{-1/2} H8 by a diagonal scaling
+        hipLaunchKernelGGL((k_flow_wave_lr<NX, NZ, TK>), dim3(grid), dim3(64), 0, s, p);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((k_flow_wave<NX, NZ, TK, OK>), dim3(grid), dim3(64), 0, s, p);
     return hipGetLastError();
   }

@@ -556,11 +556,29 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   for (int q = 0; q < TPW; ++q) {
     gacc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
     int rem = wv + q * NW, I = 0;  // pair index -> (I, J), row-major over the upper triangle
+    if (rem >= NPT) rem = 0;       // a wave with fewer pairs repeats pair 0 (its result is not stored)
     while (rem >= NT - I && I < NT) { rem -= NT - I; ++I; }
     ti[q] = I;
     tj[q] = I + rem;
   }
   const int r16 = lane & 15, kq = lane >> 4;  // A row / B column in the tile; k within the 4-row step
+  // per pair: the lane's A row / B column, clamped into the staged row (x - shift where it is a state
+  // component, the augmented 1 at NX, 0 past it) - operands by selects, no divergent branches
+  int xa_[TPW], xb_[TPW];
+  double sa_[TPW], sb_[TPW];
+  bool va_[TPW], vb_[TPW], oa_[TPW], ob_[TPW];
+#pragma unroll
+  for (int q = 0; q < TPW; ++q) {
+    const int da = 16 * ti[q] + r16, db = 16 * tj[q] + r16;
+    va_[q] = da < NX;
+    vb_[q] = db < NX;
+    oa_[q] = da == NX;
+    ob_[q] = db == NX;
+    xa_[q] = min(da, NX - 1);
+    xb_[q] = min(db, NX - 1);
+    sa_[q] = shs[xa_[q]];
+    sb_[q] = shs[xb_[q]];
+  }
   for (int c0 = 0; c0 < n; c0 += FCH) {
     const int cn = min(FCH, n - c0);
     __syncthreads();  // the previous chunk has consumed xs
@@ -580,21 +598,24 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
           wj = (fb * lws[jg]) / S;
         }
       }
-      ws[j] = wj;
+      ws[j] = wj;  // 0 past the chunk
     }
     __syncthreads();
+    // all FCH rows (rows past the chunk have weight 0 and operands 0), 4 per instruction, the wave's
+    // tile pairs interleaved (independent accumulators)
+#pragma unroll 4
+    for (int j0 = 0; j0 < FCH; j0 += 4) {
+      const int j = j0 + kq;
+      const bool live = j < cn;
+      const double wj = ws[j];
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      if (wv + q * NW >= NPT) break;  // uniform per wave
-      const int da = 16 * ti[q] + r16, db = 16 * tj[q] + r16;
-      const double sa = da < NX ? shs[da] : 0.0, sb = db < NX ? shs[db] : 0.0;
-      for (int j0 = 0; j0 < cn; j0 += 4) {
-        const int j = j0 + kq;
-        const bool live = j < cn;
-        const double wj = live ? ws[j] : 0.0;
-        const double ua = da < NX ? (live ? xs[j * XW + da] - sa : 0.0) : (da == NX ? 1.0 : 0.0);
-        const double ub = db < NX ? (live ? xs[j * XW + db] - sb : 0.0) : (db == NX && live ? 1.0 : 0.0);
-        gacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua * wj, ub, gacc[q], 0, 0, 0);
+      for (int q = 0; q < TPW; ++q) {
+        const double xa = xs[j * XW + xa_[q]] - sa_[q], xb = xs[j * XW + xb_[q]] - sb_[q];
+        double ua = va_[q] ? xa : (oa_[q] ? 1.0 : 0.0);
+        double ub = vb_[q] ? xb : (ob_[q] ? 1.0 : 0.0);
+        ua = live ? ua * wj : 0.0;
+        ub = live ? ub : 0.0;
+        gacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, gacc[q], 0, 0, 0);
       }
     }
   }

@@ -1129,6 +1129,399 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// k_flow_wave_lr: the per-particle flow of the acoustic h in the NR = NX / 2 dimensional space of
+// the targets' positions (one 64-lane workgroup per particle, persistent over particles).
+//
+// The acoustic h reads the positions only, so H = H8 E with E the NR x NX position selection and
+// H8 = dh/d(positions) (NZ x NR, NR = 8 for the joint 4-target model against NZ = 25 sensors).  With
+// R diagonal, U = R^{-1/2} H8 = Q Rq (thin Householder QR over the wave: lane k holds row k) and
+//   H8^T S^{-1} H8 = Rq^T D^{-1} Rq,  D = I + lam Rq P_pp Rq^T   (NR x NR, symmetric, eigenvalues >= 1)
+// (S = R^{1/2} (I + lam U P_pp U^T) R^{1/2}; Q^T (I + Q M Q^T)^{-1} Q = (I + M)^{-1}), so
+//   A v  = -1/2 P H^T S^{-1} H v = G v_pos,  G = -1/2 P_{:,pos} Rq^T D^{-1} Rq          (NX x NR)
+//   c    = P H^T R^{-1}(z - e) = P_{:,pos} H8^T R^{-1} (z - e)
+//   det(I + dlam A) = det(S - dlam/2 M) / det(S) = det(I + c1 Rq P_pp Rq^T) / det(D),  c1 = lam - dlam/2
+// (Sylvester; the reference's +1e-12 I retry is flow_logdet's c2 = lam - dlam / (2 (1 + eps)) form).
+// Per pseudo-time step the dense algebra is NR x NR (the QR, one Gauss-Jordan solve D X = Rq and one
+// LU log-determinant, in registers: lane c holds column c, the pivot column read with v_readlane)
+// instead of k_flow_wave's NZ x 2NZ Gauss-Jordan through LDS.  The QR keeps the algebra as accurate
+// as the reference's S solve: a Woodbury form through W = H8^T R^{-1} H8 squares the condition of H8
+// (W spans 1e-4 .. 4e5 next to a sensor) and lost 1e-10 per step; with the QR, a 40-digit
+// recomputation of the MAT golden's most ill-conditioned particle (cond S = 5e6) puts this algebra
+// at 3.7e-9 of the exact flow and the reference's own fp64 path at 3.1e-8
+// (tests/golden/flow_accuracy.py).  h and H evaluate as in k_flow_wave (identical expressions), so
+// do e = h - H eta and the weight terms.  Diagonal R only (the host takes k_flow_wave otherwise).
+template <int NX, int NZ>
+struct LrSmem {
+  static constexpr int NR = NX / 2;             // position components: x, y of each target
+  static constexpr int P = 0;                   // NX*NX  tracker covariance
+  static constexpr int XP = P + NX * NX;        // NX  x_{k-1}
+  static constexpr int GX = XP + NX;            // NX  g(x)
+  static constexpr int V = GX + NX;             // NX  v
+  static constexpr int E0 = V + NX;             // NX  eta0
+  static constexpr int ET = E0 + NX;            // NX  eta
+  static constexpr int T1 = ET + NX;            // NX
+  static constexpr int T2 = T1 + NX;            // NX
+  static constexpr int CV = T2 + NX;            // NX  c
+  static constexpr int H8 = CV + NX;            // NZ*NR  dh/d(positions)
+  static constexpr int HV = H8 + NZ * NR;       // NZ  h(eta)
+  static constexpr int ZE = HV + NZ;            // NZ  e = h(eta) - H eta
+  static constexpr int RU = ZE + NZ;            // NZ  R^{-1}(z - e)
+  static constexpr int RQ = RU + NZ;            // NR*NR  Rq (row-major, upper triangular)
+  static constexpr int R8 = RQ + NR * NR;       // NR  H8^T R^{-1}(z - e)
+  static constexpr int TT = R8 + NR;            // NR*NR  Rq P_pp
+  static constexpr int X = TT + NR * NR;        // NR*NR  D^{-1} Rq
+  static constexpr int Y = X + NR * NR;         // NR*NR  Rq^T D^{-1} Rq
+  static constexpr int G = Y + NR * NR;         // NX*NR  -1/2 P_{:,pos} Rq^T D^{-1} Rq
+  static constexpr int KS = G + NX * NR;        // NR*NZ  P_pp H8^T (S of particle 0, diagnostics)
+  static constexpr int RED = KS + NR * NZ;      // 64
+  static constexpr int SIZE = RED + 64;
+};
+
+// state index of position component a (x, y of target a / 2)
+__device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
+
+// Gauss-Jordan with partial pivoting on the NR x 2NR matrix [B | I] held column per lane (lane c < 2NR:
+// col[r] = row r of column c): -> [I | B^{-1}] (lanes NR .. 2NR - 1), log|det B|, sign.  One wave.
+template <int NR>
+__device__ __forceinline__ void lr_gauss_jordan(double (&col)[NR], double* logabs, int* sign) {
+  double la = 0.0;
+  int sg = 1;
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    double f[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) f[r] = readlane_d(col[r], p);  // the pivot column, in every lane
+    int rp = p;
+    double best = fabs(f[p]);
+#pragma unroll
+    for (int r = p + 1; r < NR; ++r)
+      if (fabs(f[r]) > best) {
+        best = fabs(f[r]);
+        rp = r;
+      }
+    if (rp != p) sg = -sg;
+#pragma unroll
+    for (int r = p + 1; r < NR; ++r)
+      if (r == rp) {  // swap rows p and rp (uniform branch)
+        const double a = col[p], fa = f[p];
+        col[p] = col[r];
+        col[r] = a;
+        f[p] = f[r];
+        f[r] = fa;
+      }
+    const double piv = f[p];
+    la += log(fabs(piv));
+    if (piv < 0.0) sg = -sg;
+    if (piv == 0.0) sg = 0;
+    const double bp = col[p] / piv;
+    col[p] = bp;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r != p) col[r] = col[r] - f[r] * bp;
+  }
+  *logabs = la;
+  *sign = sg;
+}
+
+// log|det T| and its sign by LU with partial pivoting, T NR x NR column per lane (lanes c < NR)
+template <int NR>
+__device__ __forceinline__ void lr_logdet(double (&col)[NR], double* logabs, int* sign) {
+  const int c = threadIdx.x & 63;
+  double la = 0.0;
+  int sg = 1;
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    double f[NR];
+#pragma unroll
+    for (int r = p; r < NR; ++r) f[r] = readlane_d(col[r], p);
+    int rp = p;
+    double best = fabs(f[p]);
+#pragma unroll
+    for (int r = p + 1; r < NR; ++r)
+      if (fabs(f[r]) > best) {
+        best = fabs(f[r]);
+        rp = r;
+      }
+    if (rp != p) sg = -sg;
+#pragma unroll
+    for (int r = p + 1; r < NR; ++r)
+      if (r == rp) {
+        const double a = col[p], fa = f[p];
+        col[p] = col[r];
+        col[r] = a;
+        f[p] = f[r];
+        f[r] = fa;
+      }
+    const double piv = f[p];
+    la += log(fabs(piv));
+    if (piv < 0.0) sg = -sg;
+    if (piv == 0.0) sg = 0;
+    if (c > p) {
+      const double bp = col[p] / piv;
+#pragma unroll
+      for (int r = p + 1; r < NR; ++r) col[r] = col[r] - f[r] * bp;
+    }
+  }
+  *logabs = la;
+  *sign = sg;
+}
+
+template <int NX, int NZ, int TK>
+__global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
+  static_assert(NX % 4 == 0 && NX / 2 <= 32 && NZ <= 64, "acoustic: 4 components per target, 2NR <= 64 lanes");
+  using L = Lay<NX, NZ>;
+  using SM = LrSmem<NX, NZ>;
+  constexpr int NR = SM::NR, NT = NX / 4;
+  __shared__ double sm[SM::SIZE];
+  const int t = threadIdx.x;
+  const double* __restrict__ Pm = p.Pm;
+  for (int q = t; q < NX * NX; q += 64) sm[SM::P + q] = p.Pk[q];
+  __syncthreads();
+  const double* P = sm + SM::P;
+  double* eta = sm + SM::ET;
+  double* eta0 = sm + SM::E0;
+  double* t1 = sm + SM::T1;
+  double* t2 = sm + SM::T2;
+  double* cv = sm + SM::CV;
+  double* H8 = sm + SM::H8;
+  const double psi = Pm[L::AC], d0 = Pm[L::AC + 1];
+  const double dlam = p.dlam;
+  // out[d] = (G v_pos)[d] = sum_b G[d][b] v[pos(b)]
+  auto apply_G = [&](const double* v, double* out) {
+    for (int d = t; d < NX; d += 64) {
+      double acc = 0.0;
+#pragma unroll
+      for (int b = 0; b < NR; ++b) acc += sm[SM::G + d * NR + b] * v[lr_pos(b)];
+      out[d] = acc;
+    }
+    __syncthreads();
+  };
+  for (int64_t i = blockIdx.x; i < p.N; i += gridDim.x) {
+    // ---- eta0 = g(x_{k-1}, u) + v (as k_flow_wave) ----------------------------
+    for (int d = t; d < NX; d += 64) sm[SM::XP + d] = p.x_in[(int64_t)d * p.Npad + i];
+    __syncthreads();
+    g_block<NX, NZ, TK>(sm + SM::XP, sm + SM::GX, t1, t2, Pm, p.u);
+    for (int d = t; d < NX; d += 64) {
+      double vd = 0.0;
+      if (p.noise == PF_NOISE_HOST) {
+        vd = p.v_host[i * NX + d];
+      } else if (p.noise == PF_NOISE_DEVICE) {
+        const int64_t f = i * NX + d;
+        t1[d] = pick4(normal4_bm24d(p.seed, (uint32_t)(f >> 2), 0u, p.epoch, STREAM_PROCESS), (int)(f & 3));
+      }
+      sm[SM::V + d] = vd;
+    }
+    __syncthreads();
+    if (p.noise == PF_NOISE_DEVICE) {
+      for (int d = t; d < NX; d += 64) {
+        double acc = 0.0;
+        for (int e = 0; e <= d; ++e) acc += Pm[L::LQ + d * NX + e] * t1[e];
+        sm[SM::V + d] = acc;
+      }
+      __syncthreads();
+    }
+    for (int d = t; d < NX; d += 64) {
+      const double e0 = sm[SM::GX + d] + sm[SM::V + d];
+      eta0[d] = e0;
+      eta[d] = e0;
+    }
+    __syncthreads();
+    double theta = 0.0;
+    for (int j = 0; j < p.L; ++j) {
+      const double lam = p.lams[j];
+      // ---- H8 = dh/d(positions) and h at eta (ledh.py:143-145; obs_jac_block's expressions) ----
+      for (int k = t; k < NZ; k += 64) {
+        const double sx = Pm[L::AC + 2 + k], sy = Pm[L::AC + 2 + NZ + k];
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          const double dx = eta[4 * c] - sx, dy = eta[4 * c + 1] - sy;
+          const double den = (dx * dx + dy * dy) + d0;
+          acc += psi / den;
+          const double den2 = den * den;
+          H8[k * NR + 2 * c] = (-2.0 * psi * dx) / den2;
+          H8[k * NR + 2 * c + 1] = (-2.0 * psi * dy) / den2;
+        }
+        sm[SM::HV + k] = acc;
+        double he = 0.0;  // H eta over the nonzero columns, in column order
+#pragma unroll
+        for (int a = 0; a < NR; ++a) he += H8[k * NR + a] * eta[lr_pos(a)];
+        sm[SM::ZE + k] = acc - he;  // e = h(eta) - H eta
+      }
+      __syncthreads();
+      // ---- R^{-1}(z - e), r8 = H8^T R^{-1}(z - e) --------------------------------
+      for (int k = t; k < NZ; k += 64) {
+        double acc = 0.0;
+        for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - sm[SM::ZE + l]);
+        sm[SM::RU + k] = acc;
+      }
+      // ---- Householder QR of U = R^{-1/2} H8 over the wave: lane k holds row k (NZ <= 64) -------
+      double u[NR];
+      {
+        const double rs = t < NZ ? 1.0 / sqrt(Pm[L::R + t * NZ + t]) : 0.0;
+#pragma unroll
+        for (int a = 0; a < NR; ++a) u[a] = t < NZ ? H8[t * NR + a] * rs : 0.0;
+      }
+#pragma unroll
+      for (int pc = 0; pc < NR; ++pc) {
+        const double xk = t >= pc ? u[pc] : 0.0;
+        const double nrm2 = wave_sum_ud(xk * xk);
+        const double xp = readlane_d(u[pc], pc);
+        const double alpha = xp >= 0.0 ? -sqrt(nrm2) : sqrt(nrm2);
+        const double vk = t == pc ? xp - alpha : xk;  // the reflector v (rows >= pc)
+        const double vtv = wave_sum_ud(vk * vk);
+        if (vtv > 0.0) {
+          const double beta = 2.0 / vtv;
+#pragma unroll
+          for (int c = pc + 1; c < NR; ++c) {
+            const double sc = wave_sum_ud(vk * u[c]);
+            u[c] = u[c] - beta * vk * sc;
+          }
+        }
+        u[pc] = t == pc ? alpha : (t > pc ? 0.0 : u[pc]);
+      }
+      if (t < NR)
+#pragma unroll
+        for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
+      __syncthreads();
+      for (int a = t; a < NR; a += 64) {
+        double acc = 0.0;
+        for (int k = 0; k < NZ; ++k) acc += H8[k * NR + a] * sm[SM::RU + k];
+        sm[SM::R8 + a] = acc;
+      }
+      // TT = Rq P_pp
+      for (int q = t; q < NR * NR; q += 64) {
+        const int r = q / NR, m = q - r * NR;
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < NR; ++c) acc += sm[SM::RQ + r * NR + c] * P[lr_pos(c) * NX + lr_pos(m)];
+        sm[SM::TT + q] = acc;
+      }
+      if (i == 0 && p.diagS) {  // S = lam H8 P_pp H8^T + R of particle 0 (the condition-number diagnostic)
+        for (int q = t; q < NR * NZ; q += 64) {
+          const int a = q / NZ, l = q - a * NZ;
+          double acc = 0.0;
+          for (int m = 0; m < NR; ++m) acc += P[lr_pos(a) * NX + lr_pos(m)] * H8[l * NR + m];
+          sm[SM::KS + q] = acc;
+        }
+        __syncthreads();
+        for (int q = t; q < NZ * NZ; q += 64) {
+          const int k = q / NZ, l = q - k * NZ;
+          double acc = 0.0;
+          for (int a = 0; a < NR; ++a) acc += H8[k * NR + a] * sm[SM::KS + a * NZ + l];
+          p.diagS[(int64_t)j * NZ * NZ + q] = lam * acc + Pm[L::R + q];
+        }
+      }
+      __syncthreads();
+      // ---- D = I + lam Rq P_pp Rq^T, D1 = I + c1 (..), column per lane: [D | Rq] -> [I | D^{-1} Rq] ----
+      const double c1 = lam - 0.5 * dlam;
+      double m2[NR];  // column (t mod NR) of Rq P_pp Rq^T (lanes < NR), or of Rq (lanes NR .. 2NR - 1)
+      {
+        const int cc = t < NR ? t : (t < 2 * NR ? t - NR : 0);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          double acc = 0.0;
+#pragma unroll
+          for (int m = 0; m < NR; ++m) acc += sm[SM::TT + r * NR + m] * sm[SM::RQ + cc * NR + m];
+          m2[r] = t < NR ? acc : sm[SM::RQ + r * NR + cc];
+        }
+      }
+      double colD[NR], colC[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const double id = (t < NR && r == t) ? 1.0 : 0.0;
+        colD[r] = t < NR ? id + lam * m2[r] : m2[r];  // [D | Rq]
+        colC[r] = id + c1 * m2[r];
+      }
+      double D_ld, C_ld;
+      int D_sg, C_sg;
+      lr_gauss_jordan<NR>(colD, &D_ld, &D_sg);
+      lr_logdet<NR>(colC, &C_ld, &C_sg);
+      if (C_sg * D_sg > 0) {
+        theta += C_ld - D_ld;
+      } else {  // the reference's +1e-12 I retry (ledh.py:174-179), as flow_logdet
+        const double eps = 1e-12;
+        const double c2 = lam - dlam / (2.0 * (1.0 + eps));
+#pragma unroll
+        for (int r = 0; r < NR; ++r) colC[r] = ((t < NR && r == t) ? 1.0 : 0.0) + c2 * m2[r];
+        lr_logdet<NR>(colC, &C_ld, &C_sg);
+        theta += (double)NX * log1p(eps) + C_ld - D_ld;
+      }
+      if (t >= NR && t < 2 * NR)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) sm[SM::X + r * NR + (t - NR)] = colD[r];  // D^{-1} Rq
+      __syncthreads();
+      // ---- Y = Rq^T D^{-1} Rq;  c = P_{:,pos} r8 ---------------------------------
+      for (int q = t; q < NR * NR; q += 64) {
+        const int a = q / NR, b = q - a * NR;
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc += sm[SM::RQ + r * NR + a] * sm[SM::X + r * NR + b];
+        sm[SM::Y + q] = acc;
+      }
+      for (int d = t; d < NX; d += 64) {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NR; ++a) acc += P[d * NX + lr_pos(a)] * sm[SM::R8 + a];
+        cv[d] = acc;
+      }
+      __syncthreads();
+      // ---- G = -1/2 P_{:,pos} Y ------------------------------------------------
+      for (int q = t; q < NX * NR; q += 64) {
+        const int d = q / NR, b = q - d * NR;
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NR; ++a) acc += P[d * NX + lr_pos(a)] * sm[SM::Y + a * NR + b];
+        sm[SM::G + q] = -0.5 * acc;
+      }
+      __syncthreads();
+      // ---- b = (I + 2 lam A)[(I + lam A) c + A eta0], eta += dlam (A eta + b)  (ledh.py:165-171) ----
+      apply_G(eta0, t1);  // t1 = A eta0
+      apply_G(cv, t2);    // t2 = A c
+      for (int d = t; d < NX; d += 64) t1[d] = (cv[d] + lam * t2[d]) + t1[d];  // w
+      __syncthreads();
+      apply_G(t1, t2);    // t2 = A w
+      for (int d = t; d < NX; d += 64) t1[d] = t1[d] + 2.0 * lam * t2[d];      // b
+      __syncthreads();
+      apply_G(eta, t2);   // t2 = A eta
+      for (int d = t; d < NX; d += 64) eta[d] = eta[d] + dlam * (t2[d] + t1[d]);
+      __syncthreads();
+    }
+    // ---- weight (ledh.py:186-190), as k_flow_wave ---------------------------------
+    for (int k = t; k < NZ; k += 64) {
+      const double sx = Pm[L::AC + 2 + k], sy = Pm[L::AC + 2 + NZ + k];
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        const double dx = eta[4 * c] - sx, dy = eta[4 * c + 1] - sy;
+        acc += psi / ((dx * dx + dy * dy) + d0);
+      }
+      sm[SM::HV + k] = acc;
+    }
+    __syncthreads();
+    double part = 0.0;
+    for (int d = t; d < NX; d += 64) {  // (eta - gx)^T Q^{-1} (eta - gx) - v^T Q^{-1} v
+      double a = 0.0, b = 0.0;
+      for (int e = 0; e < NX; ++e) {
+        const double qi = Pm[L::QI + d * NX + e];
+        a += qi * (eta[e] - sm[SM::GX + e]);
+        b += qi * sm[SM::V + e];
+      }
+      part += (-0.5 * ((eta[d] - sm[SM::GX + d]) * a)) - (-0.5 * (sm[SM::V + d] * b));
+    }
+    for (int k = t; k < NZ; k += 64) {
+      double a = 0.0;
+      for (int l = 0; l < NZ; ++l) a += Pm[L::RI + k * NZ + l] * (p.z[l] - sm[SM::HV + l]);
+      part += -0.5 * ((p.z[k] - sm[SM::HV + k]) * a);
+    }
+    const double tot = wave_sum64(part);
+    if (t == 0) p.lw[i] = (log(p.w_in[i] + 1e-300) + theta) + tot;
+    for (int d = t; d < NX; d += 64) p.x_out[(int64_t)d * p.Npad + i] = eta[d];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight pipeline
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double block_reduce_sum(double v, double* red) {

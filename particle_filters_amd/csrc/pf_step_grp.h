@@ -28,9 +28,6 @@ namespace pf {
 #ifndef PF_GRP_RCP
 #define PF_GRP_RCP 1
 #endif
-#ifndef PF_GRP_PF
-#define PF_GRP_PF 1  // software-pipelined particle loop (the next particle's rows in flight)
-#endif
 constexpr int SYS_STAGE = 4;  // source tiles of a block's systematic positions staged in LDS (sys_cdf)
 
 template <int NX>
@@ -570,20 +567,6 @@ k_step_grp(StepParams p) {
   const double lse_prev = h.uniform ? 0.0 : (p.use_lse_ext ? p.lse_ext : h.lse);  // shards: the global lse
   const Real lse_r = (Real)lse_prev;
   const bool write_x = p.do_predict || p.allow_gather;
-  // software pipeline (lane-local noise variants: the dense-chol(Q) ones have no registers to
-  // spare): the rows (and carried log-weight) of the group's NEXT particle are loaded while the
-  // current one is computed, so the gather's memory latency overlaps a whole pass of the
-  // Philox -> RK4 -> likelihood chain instead of opening every pass
-  constexpr bool PFE = PF_GRP_PF && QL;
-  Real xnx[PER], lnx = Real(0);
-  if constexpr (PFE) {
-    if (vt < nchunks) {
-      const int64_t src = gather ? (int64_t)anc_l[vt] : o0 + vt;
-#pragma unroll
-      for (int j = 0; j < PER; ++j) xnx[j] = x_in[(int64_t)(q * PER + j) * p.Npad + src];
-      if (!gather && p.do_update && !h.uniform) lnx = lw_in[o0 + vt];
-    }
-  }
   for (int c = vt; c < nchunks; c += VB) {
     // keep the per-lane model parameters (H rows, chol(Q) blocks, A rows) in L1 rather than
     // hoisted into ~100 VGPRs across the loop: that hoisting cost 3 of 4 waves per SIMD
@@ -591,24 +574,10 @@ k_step_grp(StepParams p) {
     const int64_t i = o0 + c;
     Real x[PER];
     Real lp = Real(0);
-    Real lcur = lnx;
-    if constexpr (PFE) {
-#pragma unroll
-      for (int j = 0; j < PER; ++j) x[j] = xnx[j];
-      const int cc = c + VB;
-      if (cc < nchunks) {
-        const int64_t src = gather ? (int64_t)anc_l[cc] : o0 + cc;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) xnx[j] = x_in[(int64_t)(q * PER + j) * p.Npad + src];
-        if (!gather && p.do_update && !h.uniform) lnx = lw_in[o0 + cc];
-      }
-    }
     if (gather) {
       const int a = anc_l[c];
-      if constexpr (!PFE) {
 #pragma unroll
-        for (int j = 0; j < PER; ++j) x[j] = x_in[(int64_t)(q * PER + j) * p.Npad + a];
-      }
+      for (int j = 0; j < PER; ++j) x[j] = x_in[(int64_t)(q * PER + j) * p.Npad + a];
       lp = (Real)lprev_uniform;
       if (p.regularize) {
         Real n[PER];
@@ -631,13 +600,9 @@ k_step_grp(StepParams p) {
         for (int j = 0; j < PER; ++j) xr[(int64_t)(q * PER + j) * p.Npad + i] = x[j];
       }
     } else {
-      if constexpr (PFE) {
-        if (p.do_update) lp = h.uniform ? (Real)lprev_uniform : lcur - lse_r;
-      } else {
 #pragma unroll
-        for (int j = 0; j < PER; ++j) x[j] = x_in[(int64_t)(q * PER + j) * p.Npad + i];
-        if (p.do_update) lp = h.uniform ? (Real)lprev_uniform : lw_in[i] - lse_r;
-      }
+      for (int j = 0; j < PER; ++j) x[j] = x_in[(int64_t)(q * PER + j) * p.Npad + i];
+      if (p.do_update) lp = h.uniform ? (Real)lprev_uniform : lw_in[i] - lse_r;
     }
     if (p.do_predict) {
       Real n[PER];
