@@ -138,7 +138,7 @@ struct LL {
   static hipError_t ekf(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
                         const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, double* Xp,
                         hipStream_t s) {
-    hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(EB), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out,
+    hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(ekf_block<NZ>()), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out,
                        Xp);
     return hipGetLastError();
   }

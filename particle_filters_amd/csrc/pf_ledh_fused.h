@@ -111,6 +111,10 @@ __device__ __forceinline__ double dpp_reduce_max(double v, double* red) {
   return s;
 }
 
+// workgroup barrier for LDS hand-offs only: unlike __syncthreads it does not wait for this wave's
+// outstanding global stores (P3's ancestors and weights keep draining under P4)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // grid barrier: every workgroup publishes `phase` in its word, then waits for all words >= phase.
 // False on timeout (the launch is abandoned and *err set; the host reports it).
 __device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long long phase) {
@@ -135,7 +139,7 @@ __device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long lo
 // in fp64; x = -inf / +inf give 0 / N).  Exactly, (U + i) / N < x <=> i < y = x N - U; the fp64
 // division can only disagree when y is within ~1e-11 of an integer, so only there are the
 // candidate positions evaluated the reference's way.
-__device__ __noinline__ int64_t fcount_exact(double x, double U, int64_t N, int64_t c) {
+__device__ __forceinline__ int64_t fcount_exact(double x, double U, int64_t N, int64_t c) {
   const double Nd = (double)N;
   while (c > 0 && (U + (double)(c - 1)) / Nd >= x) --c;
   while (c < N && (U + (double)c) / Nd < x) ++c;
@@ -345,7 +349,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       q5.finish(p, v5);
     }
   }
-  __syncthreads();
+  lds_barrier();
   LF_STAMP(1);
 
   // ---- P1: flow --------------------------------------------------------------------
@@ -386,7 +390,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     }
   }
   (void)m;
-  __syncthreads();  // every slot's log weight is in lws
+  lds_barrier();  // every slot's log weight is in lws
   LF_STAMP(12);
 
   // ---- P2: exponentials relative to the WORKGROUP max, sums and scan (no grid max needed:
@@ -488,7 +492,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       red[10] = E2;
     }
   }
-  __syncthreads();
+  lds_barrier();
   const double S = boff[FMAX];
   const double fb = red[8];
   const double lastprev = b > 0 ? red[9] : -INFINITY;
@@ -514,7 +518,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       shi[j] = (b == p.nbk - 1 && j == n - 1) ? N : fcount_below(c, U, N);
     }
     slo0 = fcount_below(lastprev, U, N);
-    __syncthreads();
+    lds_barrier();
     // slots [slo0, shi[n-1]): slot s takes the first own particle j with s < shi[j] - a binary
     // search for the thread's first slot, then a cursor (slots rise by FB per iteration: a
     // degenerate resample, one particle over most slots, costs O(1) per slot)
@@ -581,7 +585,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   }
   for (int c0 = 0; c0 < n; c0 += FCH) {
     const int cn = min(FCH, n - c0);
-    __syncthreads();  // the previous chunk has consumed xs
+    lds_barrier();  // the previous chunk has consumed xs (and shi / lws are complete)
     if (c0 > 0)  // own rows past the first flow round, from x_out
       for (int e = t; e < FCH * XW; e += FB) {
         const int j = e % FCH, d = e / FCH;
@@ -600,7 +604,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       }
       ws[j] = wj;  // 0 past the chunk
     }
-    __syncthreads();
+    lds_barrier();
     // all FCH rows (rows past the chunk have weight 0 and operands 0), 4 per instruction, the wave's
     // tile pairs interleaved (independent accumulators)
 #pragma unroll 4

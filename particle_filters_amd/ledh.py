@@ -267,6 +267,9 @@ class LEDHFlowPF:
         tr = self.tracker
         if not (isinstance(tr, TR.EKFTracker) and tr.ekf.g is self.g and tr.ekf.h is self.h):
             raise NotImplementedError("tracker='device' needs a trackers.EKFTracker over this filter's g and h")
+        if tr.ekf.jitter > 0.0 or tr.ekf.joseph:
+            raise NotImplementedError("tracker='device' runs the plain EKF update (no jitter, no Joseph form); "
+                                      "use tracker='host' for this ExtendedKalmanFilter")
         c = lambda a: np.ascontiguousarray(np.asarray(a, float))  # noqa: E731
         return c(tr.state.mean).reshape(self.nx), c(tr.state.cov).reshape(self.nx, self.nx), c(tr.ekf.Q), c(tr.ekf.R)
 

@@ -210,6 +210,19 @@ def test_run_with_device_tracker_equals_host_tracker(name):
     np.testing.assert_allclose(tr1.state.cov, tr2.state.cov, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("variant", ["jitter", "joseph"])
+def test_device_tracker_rejects_other_ekf_updates(variant):
+    """The device EKF runs the plain update (extended_kalman_filter.py:208-239 without jitter or
+    the Joseph form): an EKF configured otherwise is refused, not silently run differently."""
+    pf, tracker, ekf, g = device_tracked_filter("l96", n_particles=64)
+    if variant == "jitter":
+        ekf.jitter = 1e-9
+    else:
+        ekf.joseph = True
+    with pytest.raises(NotImplementedError, match="tracker='host'"):
+        pf.tracker_covariances(g["Z"])
+
+
 @pytest.mark.parametrize("algo", ["ledh", "edh"])
 def test_fused_step_equals_kernel_chain(algo, monkeypatch):
     """run() on the shared path uses the one-launch fused step (pf_ledh_fused.h); with
