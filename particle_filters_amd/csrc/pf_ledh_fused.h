@@ -568,16 +568,19 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   const int r16 = lane & 15, kq = lane >> 4;  // A row / B column in the tile; k within the 4-row step
   // per pair: the lane's A row / B column, clamped into the staged row (x - shift where it is a state
   // component, the augmented 1 at NX, 0 past it) - operands by selects, no divergent branches
+  // as multiply-adds: u = fma(x - shift, m, c) with (m, c) = (1, 0) for a state component, (0, 1) for
+  // the augmented 1, (0, 0) past it - the same value as the selects for finite rows, and the LDS
+  // reads stay unconditional (a select let the compiler sink each read into a branch of its own,
+  // serialising four LDS round trips per k-step)
   int xa_[TPW], xb_[TPW];
-  double sa_[TPW], sb_[TPW];
-  bool va_[TPW], vb_[TPW], oa_[TPW], ob_[TPW];
+  double sa_[TPW], sb_[TPW], ma_[TPW], mb_[TPW], ca_[TPW], cb_[TPW];
 #pragma unroll
   for (int q = 0; q < TPW; ++q) {
     const int da = 16 * ti[q] + r16, db = 16 * tj[q] + r16;
-    va_[q] = da < NX;
-    vb_[q] = db < NX;
-    oa_[q] = da == NX;
-    ob_[q] = db == NX;
+    ma_[q] = da < NX ? 1.0 : 0.0;
+    mb_[q] = db < NX ? 1.0 : 0.0;
+    ca_[q] = da == NX ? 1.0 : 0.0;
+    cb_[q] = db == NX ? 1.0 : 0.0;
     xa_[q] = min(da, NX - 1);
     xb_[q] = min(db, NX - 1);
     sa_[q] = shs[xa_[q]];
@@ -586,6 +589,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   for (int c0 = 0; c0 < n; c0 += FCH) {
     const int cn = min(FCH, n - c0);
     lds_barrier();  // the previous chunk has consumed xs (and shi / lws are complete)
+    if (c0 == 0) LF_STAMP(18);
     if (c0 > 0)  // own rows past the first flow round, from x_out
       for (int e = t; e < FCH * XW; e += FB) {
         const int j = e % FCH, d = e / FCH;
@@ -605,20 +609,18 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
       ws[j] = wj;  // 0 past the chunk
     }
     lds_barrier();
+    if (c0 == 0) LF_STAMP(19);
     // all FCH rows (rows past the chunk have weight 0 and operands 0), 4 per instruction, the wave's
     // tile pairs interleaved (independent accumulators)
-#pragma unroll 4
+#pragma unroll
     for (int j0 = 0; j0 < FCH; j0 += 4) {
       const int j = j0 + kq;
       const bool live = j < cn;
-      const double wj = ws[j];
+      const double wl = ws[j], ll = live ? 1.0 : 0.0;  // ws is 0 past the chunk
 #pragma unroll
       for (int q = 0; q < TPW; ++q) {
-        const double xa = xs[j * XW + xa_[q]] - sa_[q], xb = xs[j * XW + xb_[q]] - sb_[q];
-        double ua = va_[q] ? xa : (oa_[q] ? 1.0 : 0.0);
-        double ub = vb_[q] ? xb : (ob_[q] ? 1.0 : 0.0);
-        ua = live ? ua * wj : 0.0;
-        ub = live ? ub : 0.0;
+        const double ua = fma(xs[j * XW + xa_[q]] - sa_[q], ma_[q], ca_[q]) * wl;
+        const double ub = fma(xs[j * XW + xb_[q]] - sb_[q], mb_[q], cb_[q]) * ll;
         gacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, gacc[q], 0, 0, 0);
       }
     }

@@ -803,15 +803,35 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
 #endif
   const double part = group_trans_part<NX, NZ>(p, Pm, q, base, dd, v);
   const double* __restrict__ z = zz ? zz : p.z;
-  double ez[NZ];
+  double like;
+  if (GL > 1 && p.r_diag) {
+    // lane q of the group takes the observation components k = GL j + q: its share of the residual
+    // z - h(eta_L) and of the diagonal quadratic form, then the group sum (a quarter of the
+    // residual's QL y0 products per lane instead of all of them)
+    double lq = 0.0;
 #pragma unroll
-  for (int k = 0; k < NZ; ++k) {
-    double yl = af[T::PL + k];
+    for (int j = 0; j < (NZ + GL - 1) / GL; ++j) {
+      const int k = GL * j + q;
+      const int kc = k < NZ ? k : NZ - 1;
+      double yl = af[T::PL + kc];
 #pragma unroll
-    for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
-    ez[k] = z[k] - (yl + Pm[L::C + k]);
+      for (int l = 0; l < NZ; ++l) yl += af[T::QL + kc * NZ + l] * y0[l];
+      const double e = z[kc] - (yl + Pm[L::C + kc]);
+      const double v = e * (Pm[L::RI + kc * NZ + kc] * e);
+      lq += k < NZ ? v : 0.0;
+    }
+    like = group_sum<GL>(lq);
+  } else {
+    double ez[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+      double yl = af[T::PL + k];
+#pragma unroll
+      for (int l = 0; l < NZ; ++l) yl += af[T::QL + k * NZ + l] * y0[l];
+      ez[k] = z[k] - (yl + Pm[L::C + k]);
+    }
+    like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
   }
-  const double like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
   return (log(w_i + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
 }
 
