@@ -291,12 +291,14 @@ struct pf_ledh_handle {
   double *x = nullptr, *x_alt = nullptr, *w = nullptr, *w_alt = nullptr, *lw = nullptr;
   double *tmax = nullptr, *tsum = nullptr, *trec = nullptr, *cdf = nullptr, *stat = nullptr, *mean = nullptr;
   double* mean_prev = nullptr;  // shift of the one-pass moments (ping-pong with mean)
+  double* mean3 = nullptr;      // third mean buffer of the fused run (shift of two steps back)
   double *cpart = nullptr, *Pm = nullptr, *Pk = nullptr, *z = nullptr, *u = nullptr, *vbuf = nullptr;
   double* xbar = nullptr;  // EDH: tracker past mean of the current step
   // fused shared-path step (pf_ledh_fused.h): grid geometry, barrier words, partials
   int fused_nbk = 0, fused_ppb = 0;
   unsigned long long fphase = 0;
   unsigned long long *fwords = nullptr, *fpart = nullptr, *fcpart = nullptr;
+  int fcp = 0;  // which half of fcpart the last fused step's P4 wrote
   int32_t* fanc = nullptr;  // [N] ancestors of the slots between fused steps
   // run_impl's device buffers (tracker covariances, observations, outputs, flow tables), one
   // allocation kept across runs: a run allocates only when it needs more than the last one
@@ -526,7 +528,7 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
   struct A { double** p; size_t b; };
   A allocs[] = {{&h->x, xb}, {&h->x_alt, xb}, {&h->w, nb}, {&h->w_alt, nb}, {&h->lw, nb}, {&h->cdf, nb},
                 {&h->tmax, (size_t)h->G * 8}, {&h->tsum, (size_t)h->G * 8}, {&h->trec, (size_t)h->G * (2 + nx) * 8},
-                {&h->stat, 8 * 8}, {&h->mean, (size_t)nx * 8}, {&h->mean_prev, (size_t)nx * 8},
+                {&h->stat, 8 * 8}, {&h->mean, (size_t)nx * 8}, {&h->mean_prev, (size_t)nx * 8}, {&h->mean3, (size_t)nx * 8},
                 {&h->cpart, (size_t)h->Gc * (1 + nx + NP) * 8},
                 {&h->Pm, P.size() * 8}, {&h->Pk, (size_t)nx * nx * 8}, {&h->z, (size_t)nz * 8},
                 {&h->u, (size_t)nx * 8}, {&h->table, (size_t)TLayHost(nx, nz, h->L) * 8}, {&h->d_lams, (size_t)h->L * 8},
@@ -557,7 +559,7 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
       h->fused_nbk = (int)nbk;
       h->fused_ppb = (int)ppb;
       if (hipMalloc((void**)&h->fwords, FMAX * 8) != hipSuccess || hipMalloc((void**)&h->fpart, 4 * FMAX * 8) != hipSuccess ||
-          hipMalloc((void**)&h->fcpart, (size_t)FMAX * ops->fused_E * 8) != hipSuccess ||
+          hipMalloc((void**)&h->fcpart, 2 * (size_t)FMAX * ops->fused_E * 8) != hipSuccess ||
           hipMalloc((void**)&h->fanc, (size_t)h->N * sizeof(int32_t)) != hipSuccess ||
           hipMalloc((void**)&h->ferr, 8) != hipSuccess)
         return bail("fused step buffers");
@@ -594,7 +596,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev,
+  for (double* p : {h->x, h->x_alt, h->w, h->w_alt, h->lw, h->tmax, h->tsum, h->trec, h->cdf, h->stat, h->mean, h->mean_prev, h->mean3,
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
                     h->xbar, h->rp_noise, h->rp_unif})
     if (p) (void)hipFree(p);
@@ -916,10 +918,14 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     const bool fused_run = h->fused_nbk > 0 && dTab;
     std::optional<GridOrderScope> order;  // no overlap with another handle's grid
     if (fused_run) order.emplace(h->device, h->stream);
-    // fused path: launch t also reduces step t - 1's moments (its P5), whose mean is step t's
-    // shift; a P5-only launch ends the run.  cur: step t-1's shift buffer, oth: its mean's
-    double* cur = h->mean_prev;
-    double* oth = h->mean;
+    // fused path: launch t also reduces step t - 1's moments (its P5'); step t's moment shift is the
+    // mean of step t - 2 (the latest mean before the run for t < 2); a P5-only launch ends the run.
+    // shp: the shift step t - 1 used, shc: step t's, mw: where launch t puts the mean of step t - 1
+    double* const mbuf[3] = {h->mean_prev, h->mean, h->mean3};
+    double* shp = h->mean_prev;
+    double* shc = h->mean_prev;
+    double* mw = h->mean;
+    double* spare = h->mean3;
     // and the state between its steps is (the last step's flow rows, ancestors): xa holds the rows
     // the next step starts from, xb takes its flow rows
     double* xa = h->x;
@@ -928,7 +934,11 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       fp.stat = h->stat;
       fp.words = h->fwords;
       fp.part = h->fpart;
-      fp.cpart = h->fcpart;
+      // moment partials: P5' reads the pair's buffer the previous step's P4 wrote, P4 the other
+      const size_t cps = (size_t)FMAX * h->ops->fused_E;
+      fp.cpart5 = h->fcpart + h->fcp * cps;
+      fp.cpart = h->fcpart + (h->fcp ^ 1) * cps;
+      if (fp.step) h->fcp ^= 1;
       fp.err = h->ferr;
       fp.phase0 = h->fphase;
       h->fphase += 4;
@@ -960,13 +970,12 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         fp.step = 1;
         fp.p5 = t > 0;
         if (t > 0) {
-          fp.shift5 = cur;
-          fp.mean5 = oth;
+          fp.shift5 = shp;
+          fp.mean5 = mw;
           fp.o_mean5 = dm + (t - 1) * nx;
           fp.o_cov5 = dc + (t - 1) * nx * nx;
-          std::swap(cur, oth);
         }
-        fp.shift = cur;
+        fp.shift = shc;
         fp.o_ess = de + t;
         fp.o_flag = df + t;
         fused_common(fp);
@@ -976,6 +985,12 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
         }
         std::swap(h->w, h->w_alt);
         std::swap(xa, xb);
+        if (t > 0) {  // step t + 1: shifts (mean of t - 1 now in mw); the free buffer takes the next mean
+          double* freed = shp != shc ? shp : spare;
+          shp = shc;
+          shc = mw;
+          mw = freed;
+        }  // (t = 0: steps 0 and 1 both shift by the latest mean before the run)
         continue;
       }
       st = enqueue_flow(h, dP + t * nx * nx, dZ + t * nz, dU ? dU + t * nx : nullptr, noise,
@@ -994,14 +1009,16 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
       h->x_alt = xa;
       fp.step = 0;
       fp.p5 = 1;
-      fp.shift5 = cur;
-      fp.mean5 = oth;
+      fp.shift5 = shp;
+      fp.mean5 = mw;
       fp.o_mean5 = dm + (T - 1) * nx;
       fp.o_cov5 = dc + (T - 1) * nx * nx;
       fused_common(fp);
       if (h->ops->fused(fp, h->stream) != hipSuccess) st = lfail(PF_E_HIP, "run: fused tail launch failed");
-      h->mean_prev = oth;  // the latest mean: the next moments' shift
-      h->mean = cur;
+      h->mean_prev = mw;  // the latest mean: the next moments' shift
+      int k = 0;
+      for (double* m : mbuf)
+        if (m != mw) (k++ == 0 ? h->mean : h->mean3) = m;
     }
     if (order) order->end();
     if (ekf) (void)hipStreamSynchronize(h->side);

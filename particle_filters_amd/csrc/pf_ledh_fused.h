@@ -5,15 +5,16 @@
 // whose floors (10-17 us each on 1e4 particles, fewer waves than SIMDs) dominated config 5.
 //
 // NBK co-resident workgroups (<= one per CU), each owning PPB consecutive particles (slots):
-//   P5' the PREVIOUS step's output entries (NX + NX(NX+1)/2) over the NBK moment partials it left,
-//       spread over every workgroup; its mean is this step's moment shift (written through, read
-//       after B1).  Its loads are issued together with the parameter block's LDS staging loads.
 //   P1  flow of its slots.  The state enters as (rows, ancestors): slot i starts from row anc[i]
 //       of the previous step's flow output - the previous resample is applied by this gather, no
 //       separate copy.  Flow rows -> x_out (write-through; the first FCH also stay in LDS), log
 //       weights in LDS; the workgroup max
 //   P2  e = exp(l - m) relative to the WORKGROUP max, sum e, sum e^2 and the inclusive scan in LDS;
 //       published: (m, sum e, sum e^2, last scan value)                                   | B1
+//   P5' (waves 1.. while wave 0 runs P3's combine) the PREVIOUS step's output entries (NX +
+//       NX(NX+1)/2) over the NBK moment partials it left, spread over every workgroup; its mean is
+//       the moment shift of the NEXT step (a shift only conditions the one-pass sums: the posterior
+//       mean of two steps back serves as well as the last one, and is already in HBM at launch)
 //   P3  every workgroup combines the NBK partials in one fixed order: normaliser S, ESS,
 //       decision, the exclusive prefix O_k of the scaled workgroup sums and every workgroup's
 //       scale, hence its own CDF slice c_j = (O_b + f_b scan_j) / S (c = 1 for the last particle,
@@ -53,11 +54,11 @@ struct FusedParams {
   int32_t* anc_out;              // [N] this step's ancestors (identity without a resample)
   double* x_res;                 // tail launch: [NX][Npad] the materialised state rows[anc[i]]
   double* w_out;                 // [N] the new weights
-  const double* shift;           // [NX] this step's moment shift: the previous posterior mean (== mean5 when p5)
+  const double* shift;           // [NX] this step's moment shift: the posterior mean of two steps back
   int step;                      // 1: run a filter step; 0: a run's tail (P5' and the materialised state)
   int p5;                        // 1: reduce the previous step's moment partials (cpart) first
   const double* shift5;          // [NX] the previous step's shift
-  double* mean5;                 // [NX] the previous step's posterior mean (write-through: read after B1)
+  double* mean5;                 // [NX] the previous step's posterior mean (the shift of the next step)
   double* o_mean5;               // [NX] or null: the previous step's outputs
   double* o_cov5;                // [NX][NX] or null
   double* o_ess;                 // or null: this step's
@@ -65,7 +66,9 @@ struct FusedParams {
   double* stat;                  // [4] ess, flag, sw
   unsigned long long* words;     // [NBK] barrier phase words (monotonic across launches)
   unsigned long long* part;      // [4][FMAX] workgroup max / sum e / sum e^2 / last scan value (bits)
-  unsigned long long* cpart;     // [NBK][E] moment partials (double bits)
+  unsigned long long* cpart;     // [NBK][E] this step's moment partials (double bits), written by P4
+  const unsigned long long* cpart5;  // [NBK][E] the previous step's, read by P5' (the other buffer of a pair:
+                                     // P5' may still read while faster workgroups are past B1 in P4)
   unsigned int* err;             // barrier timeout flag
   unsigned long long phase0;     // phase word base of this launch
   double ratio;
@@ -118,8 +121,10 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // grid barrier: every workgroup publishes `phase` in its word, then waits for all words >= phase.
 // False on timeout (the launch is abandoned and *err set; the host reports it).
 __device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long long phase) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // only wave 0's stores (the published partials) must land before the phase word; the other waves'
+  // outstanding operations (flow rows for the next launch, P5' loads) are not waited for here
+  if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
   if (threadIdx.x == 0)
     __hip_atomic_store(p.words + blockIdx.x, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (unsigned spins = 0;; ++spins) {
@@ -162,17 +167,21 @@ __device__ __forceinline__ int64_t fcount_below(double x, double U, int64_t N) {
 // fixed xor tree: the same order in every run.  The partials were written by the previous launch
 // (visible after the kernel boundary): plain loads.
 constexpr int P5K = 8;  // partials per lane in one batch
-template <int NX, int FB>
+template <int NX>
 struct P5 {
   static constexpr int NOUT = NX + Mom<NX>::NP;
   int lpe, groups, gl, qo, d, e, src[4];
   bool live;
-  __device__ P5(const FusedParams& p, int round) {
-    const int t = threadIdx.x;
-    lpe = (p.nbk * (FB / 64) >= NOUT) ? 64 : (p.nbk * (FB / 32) >= NOUT ? 32 : 16);
-    groups = FB / lpe;
-    gl = t % lpe;
-    qo = (blockIdx.x + round * p.nbk) * groups + t / lpe;
+  // threads [base, base + nthr) of the workgroup (a whole number of waves) do the reduction; tid =
+  // threadIdx.x - base
+  static __device__ int lpe_of(const FusedParams& p, int nthr) {
+    return (p.nbk * (nthr / 64) >= NOUT) ? 64 : (p.nbk * (nthr / 32) >= NOUT ? 32 : 16);
+  }
+  __device__ P5(const FusedParams& p, int round, int tid, int nthr) {
+    lpe = lpe_of(p, nthr);
+    groups = nthr / lpe;
+    gl = tid % lpe;
+    qo = (blockIdx.x + round * p.nbk) * groups + tid / lpe;
     live = qo < NOUT;
     d = 0;
     e = 0;
@@ -182,13 +191,21 @@ struct P5 {
     src[2] = 1 + e;
     src[3] = qo >= NX ? 1 + NX + (qo - NX) : 0;
   }
-  static __device__ int rounds(const FusedParams& p) {
-    const int lpe = (p.nbk * (FB / 64) >= NOUT) ? 64 : (p.nbk * (FB / 32) >= NOUT ? 32 : 16);
-    const int per = p.nbk * (FB / lpe);
+  static __device__ int rounds(const FusedParams& p, int nthr) {
+    const int per = p.nbk * (nthr / lpe_of(p, nthr));
     return (NOUT + per - 1) / per;
   }
+  // all rounds of the threads [base, base + nthr)
+  static __device__ void run(const FusedParams& p, int tid, int nthr) {
+    double v[P5K][4];
+    for (int r = 0; r < rounds(p, nthr); ++r) {
+      const P5 q5(p, r, tid, nthr);
+      q5.load(p, 0, v);
+      q5.finish(p, v);
+    }
+  }
   __device__ void load(const FusedParams& p, int k0, double (&v)[P5K][4]) const {
-    const double* cp5 = (const double*)p.cpart;
+    const double* cp5 = (const double*)p.cpart5;
 #pragma unroll
     for (int r = 0; r < P5K; ++r) {
       const int k = k0 + gl + r * lpe;
@@ -269,18 +286,8 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     const int a = (t % GL) * PER + jj;
     x1[jj] = (p.step && a < NX) ? p.f.x_in[(int64_t)a * Npad + src1] : 0.0;
   }
-  double v5[P5K][4];
-  const P5<NX, FB> p5_0(p, 0);
-  if (p.p5) p5_0.load(p, 0, v5);  // issued first: its latency overlaps the staging loads below
   if (!p.step) {  // a run's tail: the last step's outputs and the materialised state rows[anc[i]]
-    if (p.p5) {
-      p5_0.finish(p, v5);
-      for (int r = 1; r < P5<NX, FB>::rounds(p); ++r) {
-        const P5<NX, FB> q5(p, r);
-        q5.load(p, 0, v5);
-        q5.finish(p, v5);
-      }
-    }
+    if (p.p5) P5<NX>::run(p, t, FB);
     if (p.anc_in)
       for (int e = t; e < n * NX; e += FB) {
         const int j = e % n, d = e / n;
@@ -295,6 +302,9 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   // over (H, D, QL, ... at lane-dependent offsets): copied once per workgroup into LDS, so the
   // per-particle chain waits on LDS instead of L2 round trips at one wave per SIMD.  Only the parts
   // the flow reads (the diagonals of chol(Q) and Q^{-1} when Q is diagonal), in batches of loads.
+  // (Tried: the first flow round's prior under the staging loads - slower, 25.7 -> 27.1 us: its
+  // chol(Q) loads queue behind the staging loads in vmcnt order.)
+  const int q = t % GL, slot = t / GL, base = lane - q;
   {
     const bool qd = p.f.q_diag != 0;
     constexpr int nA = TK != PF_TRANS_L96 ? NX * NX : 0;
@@ -341,32 +351,26 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     }
   }
   if (t < NZ) zs[t] = p.f.z[t];
-  if (p.p5) {  // the previous step's outputs and mean (= this step's shift)
-    p5_0.finish(p, v5);
-    for (int r = 1; r < P5<NX, FB>::rounds(p); ++r) {
-      const P5<NX, FB> q5(p, r);
-      q5.load(p, 0, v5);
-      q5.finish(p, v5);
-    }
-  }
+  // P4's moment shift: the posterior mean of two steps back (written by the previous launch)
+  if (t < NX) shs[t] = p.shift[t];
   lds_barrier();
   LF_STAMP(1);
 
   // ---- P1: flow --------------------------------------------------------------------
   double m = -INFINITY;
   {
-    const int q = t % GL, slot = t / GL, base = lane - q;
     for (int c0 = 0; c0 < n; c0 += FCH) {
       const int j = c0 + slot;
       const bool live = j < n;
       // whole lane groups stay together; dead groups run particle i0 (results discarded)
       const int64_t i = live ? i0 + j : i0;
-      // the previous step's resample: the slot starts from its ancestor's row
+      // the previous step's resample: the slot starts from its ancestor's row (the first round's row
+      // and weight were loaded at entry)
       const int64_t src = c0 == 0 ? src1 : (p.anc_in ? (int64_t)p.anc_in[i] : i);
       const double wi = c0 == 0 ? w1 : p.f.w_in[i];
-      double eta[PER];
-      const double l =
-          flow_affine_particle<NX, NZ, TK>(p.f, pms, afs, i, src, q, base, eta, wi, x1, zs, c0 == 0);
+      double eta[PER], gx[PER], v[PER];
+      group_prior<NX, NZ, TK>(p.f, pms, i, src, q, base, gx, v, x1, c0 == 0);
+      const double l = flow_affine_post<NX, NZ, TK>(p.f, pms, afs, q, base, gx, v, eta, wi, zs);
 #ifdef PF_STAMPS
       asm volatile("" ::"v"(l));
       if (c0 == 0) LF_STAMP(11);
@@ -438,19 +442,30 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   }
   LF_STAMP(13);
   LF_STAMP(2);
+  // P5' (waves 1..): the previous step's moment partials (written by the previous launch) are loaded
+  // before the grid barrier, so their latency hides under the wait
+  const P5<NX> q5(p, 0, t - 64, FB - 64);
+  double v5[P5K][4];
+  if (wv != 0 && p.p5) q5.load(p, 0, v5);
   if (!f_barrier(p, ph + 1)) return;
   LF_STAMP(3);
 
   // ---- P3: global normaliser, ESS, decision; this slice of the CDF; the ancestors -----------
-  // P4's moment shift is loaded here with the partials: one round trip for both
-  // P4's moment shift (the previous posterior mean, written by P5' of other workgroups this launch:
-  // write-through loads after B1) staged in LDS with the combine's results
-  if (t < NX) shs[t] = f_ldd(p.shift + t);
   // the NBK partials combined by one wave (lane l: workgroups KL l .. KL l + KL - 1) in one fixed
   // order, so every workgroup derives the same normaliser, ESS, decision and CDF slices; one
-  // barrier hands the results to the other waves
+  // barrier hands the results to the other waves.  Meanwhile the other waves reduce the previous
+  // step's moment partials (P5').
   LF_STAMP(14);
-  if (wv == 0) {
+  if (wv != 0) {
+    if (p.p5) {
+      q5.finish(p, v5);
+      for (int r = 1; r < P5<NX>::rounds(p, FB - 64); ++r) {
+        const P5<NX> r5(p, r, t - 64, FB - 64);
+        r5.load(p, 0, v5);
+        r5.finish(p, v5);
+      }
+    }
+  } else {
     constexpr int KL = FMAX / 64;
     double mk[KL], sk[KL], s2k[KL], slk[KL];
 #pragma unroll
@@ -585,6 +600,10 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     xb_[q] = min(db, NX - 1);
     sa_[q] = shs[xa_[q]];
     sb_[q] = shs[xb_[q]];
+  }
+  if (n > FCH) {  // rows past the first flow round are read back from x_out: every wave's stores done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
   }
   for (int c0 = 0; c0 < n; c0 += FCH) {
     const int cn = min(FCH, n - c0);

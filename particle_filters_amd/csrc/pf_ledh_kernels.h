@@ -747,17 +747,16 @@ __device__ __forceinline__ double wt_load(const double* p) {
 // w_i = w_in[i], loaded by the caller ahead of the chain.
 // Pm: the parameter block (Lay), af: the composed flow (TLay::aff) - p.Pm / p.table in HBM, or
 // copies staged in LDS (k_ledh_fused).
+// The part after the prior (gx = g(x), v its process noise): split from flow_affine_particle so that
+// k_ledh_fused can run the prior while its LDS staging loads are in flight.
 template <int NX, int NZ, int TK>
-__device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
-                                                      const double* __restrict__ af, int64_t i, int64_t src, int q,
-                                                      int base, double* eta, double w_i,
-                                                      const double* xpre = nullptr, const double* zz = nullptr,
-                                                      bool use_pre = false) {
+__device__ __forceinline__ double flow_affine_post(const FlowParams& p, const double* __restrict__ Pm,
+                                                  const double* __restrict__ af, int q, int base, const double* gx,
+                                                  const double* v, double* eta, double w_i,
+                                                  const double* zz = nullptr) {
   using L = Lay<NX, NZ>;
   using T = TLay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
-  double gx[PER], v[PER];
-  group_prior<NX, NZ, TK>(p, Pm, i, src, q, base, gx, v, xpre, use_pre);
 #ifdef PF_STAMPS
   asm volatile("" ::"v"(v[PER - 1]), "v"(gx[PER - 1]));
   LF_STAMP(8);
@@ -833,6 +832,16 @@ __device__ __forceinline__ double flow_affine_particle(const FlowParams& p, cons
     like = quad_form<NZ>(ez, Pm + L::RI, p.r_diag != 0);
   }
   return (log(w_i + 1e-300) + af[T::TH]) + (part + (-0.5 * like));
+}
+
+template <int NX, int NZ, int TK>
+__device__ __forceinline__ double flow_affine_particle(const FlowParams& p, const double* __restrict__ Pm,
+                                                      const double* __restrict__ af, int64_t i, int64_t src, int q,
+                                                      int base, double* eta, double w_i) {
+  constexpr int PER = Grp<NX>::PER;
+  double gx[PER], v[PER];
+  group_prior<NX, NZ, TK>(p, Pm, i, src, q, base, gx, v);
+  return flow_affine_post<NX, NZ, TK>(p, Pm, af, q, base, gx, v, eta, w_i);
 }
 
 template <int NX, int NZ, int TK>

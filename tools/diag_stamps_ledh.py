@@ -24,7 +24,7 @@ pf = LD.LEDHFlowPF(tr, g, h, h.jacobian, M.GaussianTransitionDensity(g, Q), M.Ga
                    LD.LEDHConfig(n_particles=Np, n_lambda_steps=8, resample_ess_ratio=0.5,
                                  rng=np.random.default_rng(1)), rng_mode="device")
 st = pf.init_from_gaussian(m0, c0)
-names = {0: "entry", 1: "P5 prev step", 6: " flow: x loaded", 7: " flow: RK4", 8: " flow: noise", 9: " flow: H eta0", 10: " flow: eta_L", 11: " flow: weight", 12: " P1 rows out + wg max", 13: " P2 exp + scan", 2: "P1+P2 flow/exp", 3: "B1", 14: " P3 partials loaded", 15: " P3 combine + decision", 4: "P3 decide", 18: " P4 setup + chunk barrier", 19: " P4 weights staged", 16: " P4 MFMA Gram accumulate", 17: " P4 partial stores", 5: "P4 rows+moments"}
+names = {0: "entry", 1: "params staged (first prior under it)", 6: " flow: x loaded", 7: " flow: RK4", 8: " flow: noise", 9: " flow: H eta0", 10: " flow: eta_L", 11: " flow: weight", 12: " P1 rows out + wg max", 13: " P2 exp + scan", 2: "P1+P2 flow/exp", 3: "B1", 14: " P3 partials loaded", 15: " P3 combine + decision", 4: "P3 decide", 18: " P4 setup + chunk barrier", 19: " P4 weights staged", 16: " P4 MFMA Gram accumulate", 17: " P4 partial stores", 5: "P4 rows+moments"}
 FST = 20
 for T in (10, 30, 50):
     res = pf.run(pf.state, sim.observations[1:T + 1], tracker="device", process_noise=noise)
