@@ -384,6 +384,12 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
         }
         if (q == 0) lws[j] = l;
         m = fmax(m, l);
+      } else if (c0 == 0) {  // a slot past the workgroup's particles: a zero row for P4's products
+#pragma unroll
+        for (int jj = 0; jj < PER; ++jj) {
+          const int a = q * PER + jj;
+          if (a < XW) xs[j * XW + a] = 0.0;
+        }
       }
     }
     if constexpr (GL * PER < XW) {  // pad columns past the lane groups' components

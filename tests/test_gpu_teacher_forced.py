@@ -33,7 +33,7 @@ Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the 
                             one particle), and of the oracle's set within that + 4 |dx| / sigma
 The kernels covered: k_resident (config 2, N = 1e6), k_step_grp<float,40,10> (config 3, N = 1e5),
 k_step_grp<float,16,25> (config 4, 8 x 1e5: lane-local transition, v_rcp_f32 acoustic terms,
-rounds-aware tiles), k_step<float,1,1> over 64 x 1e6 (sv64) and k_step<double,1,1> (the fp64 line,
+rounds-aware tiles), k_step_stream over 64 x 1e6 (sv64) and k_step<double,1,1> (the fp64 line,
 at 1e-12 tolerances).
 Every boundary's measured quantities and bounds go to $PF_EVIDENCE_DIR (default gpurun_out/evidence)
 as teacher_forced_<workload>.json (the round's copy is kept under profiles/).
@@ -68,7 +68,8 @@ def _boundaries(T, n, flags_hint=None, seed=3):
     return sorted(b)
 
 
-def chain(name, T, n_bound=20, reps=None, precision="fp32", expect_resident=None, tol=None, step_kw=None):
+def chain(name, T, n_bound=20, reps=None, precision="fp32", expect_resident=None, tol=None, step_kw=None,
+          expect_streamed=None):
     wl = bench.WORKLOADS[name]()
     g, h, Q, R, Z, truth, mean0, cov0 = wl.build(T, 0)
     Q, R = np.asarray(Q, float), np.asarray(R, float)
@@ -99,6 +100,8 @@ def chain(name, T, n_bound=20, reps=None, precision="fp32", expect_resident=None
         r = pf.run(Z[t:t + 1])
         if expect_resident is not None:
             assert pf.last_run_resident == expect_resident
+        if expect_streamed is not None:  # the boundary step ran on k_step_stream (or not)
+            assert bool(NV.load().pf_last_step_streamed(pf.handle)) == expect_streamed
         seg_means[t] = r.means[0]
         xe_post = pf.particles()
         for k in (reps if len(reps) <= 8 else reps[bi % len(reps)::max(1, len(reps) // 4)][:2]):
@@ -168,9 +171,10 @@ def test_step_grp_mat_config4():
 
 
 def test_step_sv64():
-    """k_step<float,1,1> over 64 x 1e6 (SURVEY 8(d) roofline run), T = 100; 2 replicates checked per
-    boundary, rotating over the 64."""
-    _, same = chain("sv64", 100, n_bound=8, reps=list(range(64)))
+    """64 x 1e6 (SURVEY 8(d) roofline run), T = 100: the shipped kernel for these fused steps is the
+    persistent k_step_stream (asserted at every boundary step; the segmented chain is also bitwise the
+    uninterrupted run); 2 replicates checked per boundary, rotating over the 64."""
+    _, same = chain("sv64", 100, n_bound=8, reps=list(range(64)), expect_streamed=True)
     assert same
 
 
