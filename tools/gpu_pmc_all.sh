@@ -1,7 +1,7 @@
 #!/bin/bash
 # Every bench line's PMC passes at HEAD (FETCH_SIZE, WRITE_SIZE, SQ issue counters; separate runs,
 # no trace domains - MI355X_MICROARCH.md HBM section), plus rocprofv3 kernel statistics of each
-# line.  Fold on the build host with tools/pmc_fold_r04.py.   tools/gpu_pmc_all.sh OUTDIR [workload...]
+# line.  Fold on the build host with tools/pmc_fold.py.   tools/gpu_pmc_all.sh OUTDIR [workload...]
 D=${1:-gpurun_out/pmc}
 mkdir -p "$D"; . "$(dirname "$0")/gpu_lib.sh"
 ISSUE="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"

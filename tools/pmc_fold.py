@@ -1,7 +1,9 @@
-"""Fold the PMC passes of tools/gpu_pmc_all.sh into profiles/pmc_*.json (read by bench.py) and copy
-the raw counter files under profiles/r04/pmc/.
+"""Fold the PMC passes of tools/gpu_pmc_all.sh / gpu_pmc.sh into profiles/pmc_*.json (read by bench.py)
+and copy the raw counter files under profiles/<round>/pmc/.
 
-    python tools/pmc_fold_r04.py gpurun_out/<pmc dir>
+    python tools/pmc_fold.py gpurun_out/<pmc dir> <round, e.g. r05> [name=K,W ...]
+
+(name=K,W overrides the bench line's timed steps K and warm-up W the profiled run used.)
 
 Per workload: FETCH_SIZE / WRITE_SIZE per launch of the bench line's dominant kernel (separate
 passes, tools/pmc_summary.py: KiB -> B, FETCH doubled on gfx950), summed over its launches and
@@ -16,7 +18,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 D = sys.argv[1]
-OUT = os.path.join(REPO, "profiles", "r04", "pmc")
+RND = sys.argv[2] if len(sys.argv) > 2 else "r05"
+OUT = os.path.join(REPO, "profiles", RND, "pmc")
 os.makedirs(OUT, exist_ok=True)
 
 # filter steps the profiled bench run covers: the warm-up W and the timed K, plus (nx > 4 with the
@@ -29,8 +32,12 @@ LINES = {
     "sv_fp64": (20, 5, "k_step<double, 1, 1", "k_step", 1, 1024),
     "l96": (50, 5, "k_step_grp<float, 40, 10", "k_step_grp", 1, 1024),
     "mat": (40, 4, "k_step_grp<float, 16, 25", "k_step_grp", 1, 1024),
-    "ledh": (50, 5, "k_ledh_fused", "k_ledh_fused", 1, 628),  # 157 one-wave-per-SIMD workgroups
+    "ledh": (200, 20, "k_ledh_fused", "k_ledh_fused", 1, 628),  # 157 one-wave-per-SIMD workgroups
 }
+for arg in sys.argv[3:]:  # name=K,W
+    nm, kw = arg.split("=")
+    k_, w_ = (int(v) for v in kw.split(","))
+    LINES[nm] = (k_, w_) + LINES[nm][2:]
 OUTNAME = {"sv": "pmc_traffic.json"}
 
 
@@ -81,10 +88,10 @@ for name, (K, W, kern, short, spl, simds) in LINES.items():
         d = json.load(open(outj))
         d["source"] = (f"rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES "
                        f"({name}); 2 cycles per wave VALU issue, 2.4 GHz; per-dispatch sums in "
-                       f"{os.path.relpath(dst_csv, REPO)} (tools/gpu_pmc_all.sh, tools/pmc_fold_r04.py)")
+                       f"{os.path.relpath(dst_csv, REPO)} (tools/gpu_pmc_all.sh, tools/pmc_fold.py)")
         json.dump(d, open(outj, "w"), indent=1)
     st = first(f"{D}/{name}_stats/**/*results.db")
     if st:  # rocprofv3 --kernel-trace --stats of the same line: per-kernel statistics (tools/rocpd_stats.py)
         subprocess.run([sys.executable, os.path.join(REPO, "tools", "rocpd_stats.py"), st,
                         os.path.join(OUT, f"{name}_kernel_stats.csv")], check=True, cwd=REPO, stdout=subprocess.DEVNULL)
-print("folded into profiles/pmc_*.json; raw files under profiles/r04/pmc/")
+print(f"folded into profiles/pmc_*.json; raw files under profiles/{RND}/pmc/")
