@@ -19,6 +19,7 @@
 
 #include "../../include/pf_engine.h"
 #include "pf_cov.h"
+#include "pf_hooks.h"
 #include "pf_order.h"
 #include "../../include/pf_shard.h"
 #include "pf_diag.h"
@@ -794,8 +795,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   // on this handle, or with PF_COOP=1.
   const char* coop_env = std::getenv("PF_COOP");
   const bool coop = (coop_env && std::atoi(coop_env) == 1) || h->res_force_coop || Rg < h->R;
-  const char* ta = std::getenv("PF_TEST_ABORT");
-  q.test_abort = (ta && std::atoi(ta) == 1 && !coop) ? 1 : 0;
+  q.test_abort = (test_hook("PF_TEST_ABORT") && !coop) ? 1 : 0;  // test hook (pf_hooks.h)
   // Resident launches of different handles (streams) on one device never overlap: two grids that
   // each hold part of the CUs would wait for each other's missing workgroups.
   GridOrderScope order(h->device, h->stream);

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/pf_ledh.h"
+#include "pf_hooks.h"
 #include "pf_ledh_ekf.h"
 #include "pf_ledh_kernels.h"
 #include "pf_diag.h"
@@ -785,11 +786,9 @@ struct EkfSpec {
 // The T loop (pf_ledh_run / pf_ledh_run_ekf): tracker covariances from the host (Ps) or from the
 // device EKF, all flow tables built up front, then flow -> weights -> resample -> moments per step.
 // EDH handles also take the tracker's past means Xb [T][nx] (host) or get them from the device EKF.
-// test hook: PF_TEST_LEDH_FAIL=1 reports the fused grid barrier as timed out after a completed run
-bool test_barrier_fail() {
-  const char* e = std::getenv("PF_TEST_LEDH_FAIL");
-  return e && std::atoi(e) == 1;
-}
+// test hook (pf_hooks.h): PF_TEST_LEDH_FAIL=1 reports the fused grid barrier as timed out after a
+// completed run
+bool test_barrier_fail() { return pf::test_hook("PF_TEST_LEDH_FAIL"); }
 
 pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const EkfSpec* ekf, const double* Z,
                    const double* U, int64_t T, int32_t noise, double* means, double* covs, double* ess,

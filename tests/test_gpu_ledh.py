@@ -276,6 +276,7 @@ def test_fused_run_failure_poisons_handle(monkeypatch):
     st = pf.init_from_gaussian(g["mean0"], g["cov0"])
     Z = np.asarray(g["Z"], float)
     pf.run(st, Z[:3], tracker="device")  # a good run first
+    monkeypatch.setenv("PF_TEST_HOOKS", "1")
     monkeypatch.setenv("PF_TEST_LEDH_FAIL", "1")
     with pytest.raises(Exception) as e:
         pf.run(pf.state, Z[3:6], tracker="device")

@@ -76,6 +76,7 @@ def test_plain_and_cooperative_are_bitwise_equal(data, monkeypatch):
 def test_host_run_repeats_an_aborted_launch(data, monkeypatch):
     x0, Z = data
     ref = host_run(x0, Z)
+    monkeypatch.setenv("PF_TEST_HOOKS", "1")
     monkeypatch.setenv("PF_TEST_ABORT", "1")
     got = host_run(x0, Z)
     same(ref, got)
@@ -99,6 +100,7 @@ def test_abort_with_two_replicates_repeats_bitwise(data, monkeypatch):
 
     monkeypatch.delenv("PF_TEST_ABORT", raising=False)
     ref = run()
+    monkeypatch.setenv("PF_TEST_HOOKS", "1")
     monkeypatch.setenv("PF_TEST_ABORT", "1")
     got = run()
     same(ref, got)
@@ -146,6 +148,7 @@ def test_device_run_abort_leaves_the_state_unchanged(data, monkeypatch):
     run = DeviceRun(pf, Z)
     run.launch(0, 20)  # a clean first part
     run.sync()
+    monkeypatch.setenv("PF_TEST_HOOKS", "1")
     monkeypatch.setenv("PF_TEST_ABORT", "1")
     run.launch(20, T)
     with pytest.raises(NV.PFRetry):
