@@ -1,5 +1,5 @@
 """Per-phase timing of k_step from s_memrealtime stamps (PF_STAMPS build).
-usage: PF_LIB=build/libpf_hip_stamps.so python tools/diag_stamps.py [N]"""
+usage: PF_LIB=build/libpf_hip_stamps.so python tools/diag_stamps.py [N] [fp32|fp64]"""
 import os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -9,7 +9,9 @@ from particle_filters_amd.batch import ParticleFilterBatch
 lib = NV.load()
 lib.pf_debug_stamps_sv.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 Np = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
-pf = ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]], Np=Np, seed=1)
+prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+pf = ParticleFilterBatch(M.SVTransition(0.95), M.SVLogSqObservation(1.0), [[0.04]], [[M.LOGCHI2_VAR]], Np=Np, seed=1,
+                         precision=prec)
 pf.initialize([0.0], [[0.5]])
 G, tile, lds = pf.geometry()
 d = S.simulate_sv_1d(400, 0.95, 0.2, 1.0, seed=42)
