@@ -298,7 +298,7 @@ struct pf_ledh_handle {
   // fused shared-path step (pf_ledh_fused.h): grid geometry, barrier words, partials
   int fused_nbk = 0, fused_ppb = 0;
   unsigned long long fphase = 0;
-  unsigned long long *fwords = nullptr, *fpart = nullptr, *fcpart = nullptr;
+  unsigned long long *fpart = nullptr, *fcpart = nullptr;
   int fcp = 0;  // which half of fcpart the last fused step's P4 wrote
   int32_t* fanc = nullptr;  // [N] ancestors of the slots between fused steps
   // run_impl's device buffers (tracker covariances, observations, outputs, flow tables), one
@@ -559,12 +559,12 @@ static pf_status create_impl(const pf_model_desc* m, const pf_ledh_opts* o, int 
     if (want && nbk <= FMAX && nbk <= (int64_t)per_cu * cus) {
       h->fused_nbk = (int)nbk;
       h->fused_ppb = (int)ppb;
-      if (hipMalloc((void**)&h->fwords, FMAX * 8) != hipSuccess || hipMalloc((void**)&h->fpart, 4 * FMAX * 8) != hipSuccess ||
+      if (hipMalloc((void**)&h->fpart, 8 * FMAX * 8) != hipSuccess ||
           hipMalloc((void**)&h->fcpart, 2 * (size_t)FMAX * ops->fused_E * 8) != hipSuccess ||
           hipMalloc((void**)&h->fanc, (size_t)h->N * sizeof(int32_t)) != hipSuccess ||
           hipMalloc((void**)&h->ferr, 8) != hipSuccess)
         return bail("fused step buffers");
-      (void)hipMemset(h->fwords, 0, FMAX * 8);
+      (void)hipMemset(h->fpart, 0, 8 * FMAX * 8);  // tag 0: never a launch's (tags start at 1)
       (void)hipMemset(h->ferr, 0, 8);
     }
   }
@@ -601,7 +601,7 @@ void pf_ledh_destroy(pf_ledh_handle* h) {
                     h->cpart, h->Pm, h->Pk, h->z, h->u, h->vbuf, h->table, h->d_lams, h->diagS, h->out, h->unif, h->Lc,
                     h->xbar, h->rp_noise, h->rp_unif})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)h->fwords, (void*)h->fpart, (void*)h->fcpart, (void*)h->fanc, (void*)h->ferr, (void*)h->arena})
+  for (void* p : {(void*)h->fpart, (void*)h->fcpart, (void*)h->fanc, (void*)h->ferr, (void*)h->arena})
     if (p) (void)hipFree(p);
   if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->side) (void)hipStreamDestroy(h->side);
@@ -931,7 +931,6 @@ pf_status run_impl(pf_ledh_handle* h, const double* Ps, const double* Xb, const 
     double* xb = h->x_alt;
     auto fused_common = [&](FusedParams& fp) {
       fp.stat = h->stat;
-      fp.words = h->fwords;
       fp.part = h->fpart;
       // moment partials: P5' reads the pair's buffer the previous step's P4 wrote, P4 the other
       const size_t cps = (size_t)FMAX * h->ops->fused_E;

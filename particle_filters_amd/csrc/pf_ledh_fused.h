@@ -64,13 +64,13 @@ struct FusedParams {
   double* o_ess;                 // or null: this step's
   int32_t* o_flag;               // or null
   double* stat;                  // [4] ess, flag, sw
-  unsigned long long* words;     // [NBK] barrier phase words (monotonic across launches)
-  unsigned long long* part;      // [4][FMAX] workgroup max / sum e / sum e^2 / last scan value (bits)
+  unsigned long long* part;      // [8][FMAX] granules {32-bit tag, 32-bit half} of the workgroup max /
+                                 // sum e / sum e^2 / last scan value (hi, lo halves of each double)
   unsigned long long* cpart;     // [NBK][E] this step's moment partials (double bits), written by P4
   const unsigned long long* cpart5;  // [NBK][E] the previous step's, read by P5' (the other buffer of a pair:
                                      // P5' may still read while faster workgroups are past B1 in P4)
   unsigned int* err;             // barrier timeout flag
-  unsigned long long phase0;     // phase word base of this launch
+  unsigned long long phase0;     // tag base of this launch (monotonic across launches)
   double ratio;
   uint32_t ep_res;               // Philox epoch of the resampling offset U
   const double* rp_unif;         // replayed U of this step (host draw stream) or null (Philox)
@@ -118,26 +118,19 @@ __device__ __forceinline__ double dpp_reduce_max(double v, double* red) {
 // outstanding global stores (P3's ancestors and weights keep draining under P4)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// grid barrier: every workgroup publishes `phase` in its word, then waits for all words >= phase.
-// False on timeout (the launch is abandoned and *err set; the host reports it).
-__device__ __forceinline__ bool f_barrier(const FusedParams& p, unsigned long long phase) {
-  // only wave 0's stores (the published partials) must land before the phase word; the other waves'
-  // outstanding operations (flow rows for the next launch, P5' loads) are not waited for here
-  if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(p.words + blockIdx.x, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (unsigned spins = 0;; ++spins) {
-    int good = 1;
-    if ((int)threadIdx.x < p.nbk)
-      good = __hip_atomic_load(p.words + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= phase;
-    if (__syncthreads_and(good)) return true;
-    if (spins >= FSPIN || __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-      if (threadIdx.x == 0) atomicOr(p.err, 1u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
+// The grid hand-off (B1) is the partials themselves: each double is published as two 64-bit granules
+// {tag, 32-bit half} (one atomic store each, no fence and no separate phase word), and a reader takes a
+// workgroup's partials once all 8 of its granules carry this launch's tag - one round trip instead of
+// store completion + phase word + poll + reload.  Tags are the launch's phase base + 1 (the host
+// advances it per launch), so the buffer never needs clearing.
+__device__ __forceinline__ void g_pub(unsigned long long* p, unsigned tag, unsigned pay) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | pay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long g_ld(const unsigned long long* p) {
+  return __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double g_double(unsigned long long hi, unsigned long long lo) {
+  return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
 }
 
 // #{ i in [0, N) : (U + i) / N < x } with the destination search's comparison (pos = (U + i) / N
@@ -439,11 +432,10 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     const double S_b = lane63_d(inc);
     const double S2_b = wave_sum_ud(s2);
     last = readlane_d(last, (n - 1) / PL);  // scan[n - 1], the value this workgroup's slice ends on
-    if (lane == 0) {
-      f_st(p.part + 0 * FMAX + b, mw);
-      f_st(p.part + 1 * FMAX + b, S_b);
-      f_st(p.part + 2 * FMAX + b, S2_b);
-      f_st(p.part + 3 * FMAX + b, last);
+    if (lane < 8) {  // granule g = lane: value g / 2, high half for even g
+      const double val = lane < 2 ? mw : (lane < 4 ? S_b : (lane < 6 ? S2_b : last));
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(val);
+      g_pub(p.part + lane * FMAX + b, (unsigned)(p.phase0 + 1), (lane & 1) ? (unsigned)bits : (unsigned)(bits >> 32));
     }
   }
   LF_STAMP(13);
@@ -453,8 +445,6 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
   const P5<NX> q5(p, 0, t - 64, FB - 64);
   double v5[P5K][4];
   if (wv != 0 && p.p5) q5.load(p, 0, v5);
-  if (!f_barrier(p, ph + 1)) return;
-  LF_STAMP(3);
 
   // ---- P3: global normaliser, ESS, decision; this slice of the CDF; the ancestors -----------
   // the NBK partials combined by one wave (lane l: workgroups KL l .. KL l + KL - 1) in one fixed
@@ -473,15 +463,39 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     }
   } else {
     constexpr int KL = FMAX / 64;
+    // B1: poll the granules of workgroups KL lane .. KL lane + KL - 1 until all carry this launch's tag
+    const unsigned tag = (unsigned)(ph + 1);
+    unsigned long long gv[KL][8];
+    bool ok_b1 = true;
+    for (unsigned spins = 0;; ++spins) {
+      bool good = true;
+#pragma unroll
+      for (int k = 0; k < KL; ++k) {
+        const int kk = KL * lane + k;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          gv[k][g] = kk < p.nbk ? g_ld(p.part + g * FMAX + kk) : ((unsigned long long)tag << 32);
+          good &= (unsigned)(gv[k][g] >> 32) == tag;
+        }
+      }
+      if (__all(good)) break;
+      if (spins >= FSPIN || __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        if (lane == 0) atomicOr(p.err, 1u);
+        ok_b1 = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) red[11] = ok_b1 ? 1.0 : 0.0;
+    LF_STAMP(3);
     double mk[KL], sk[KL], s2k[KL], slk[KL];
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
-      const int kk = KL * lane + k;
-      const bool ok = kk < p.nbk;
-      mk[k] = ok ? f_ld(p.part + 0 * FMAX + kk) : -INFINITY;
-      sk[k] = ok ? f_ld(p.part + 1 * FMAX + kk) : 0.0;
-      s2k[k] = ok ? f_ld(p.part + 2 * FMAX + kk) : 0.0;
-      slk[k] = ok ? f_ld(p.part + 3 * FMAX + kk) : 0.0;
+      const bool ok = KL * lane + k < p.nbk;
+      mk[k] = ok ? g_double(gv[k][0], gv[k][1]) : -INFINITY;
+      sk[k] = ok ? g_double(gv[k][2], gv[k][3]) : 0.0;
+      s2k[k] = ok ? g_double(gv[k][4], gv[k][5]) : 0.0;
+      slk[k] = ok ? g_double(gv[k][6], gv[k][7]) : 0.0;
     }
     double ml = -INFINITY;
 #pragma unroll
@@ -514,6 +528,7 @@ __global__ void __launch_bounds__(FusedBlk<NX>::FB) k_ledh_fused(FusedParams p) 
     }
   }
   lds_barrier();
+  if (red[11] == 0.0) return;  // B1 timed out (the host reports it)
   const double S = boff[FMAX];
   const double fb = red[8];
   const double lastprev = b > 0 ? red[9] : -INFINITY;
