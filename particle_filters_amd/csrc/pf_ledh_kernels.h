@@ -602,6 +602,10 @@ __device__ __forceinline__ void group_prior(const FlowParams& p, const double* _
                                             bool use_pre = false) {
   using L = Lay<NX, NZ>;
   constexpr int GL = Grp<NX>::GL, PER = Grp<NX>::PER;
+  // the process noise's normals depend on (particle, epoch) only: drawn first, so the Philox
+  // arithmetic runs while the row loads are in flight
+  double nrm[PER];
+  if (p.noise == PF_NOISE_DEVICE) normals_range<PER>(p.seed, i * NX + q * PER, p.epoch, STREAM_PROCESS, nrm);
   // xpre (when given) always points at the caller's register array and use_pre picks its values:
   // a pointer chosen at run time between that array and null would force the array into scratch
   double x[PER];
@@ -682,8 +686,7 @@ __device__ __forceinline__ void group_prior(const FlowParams& p, const double* _
       v[j] = a < NX ? p.v_host[i * NX + a] : 0.0;
     }
   } else if (p.noise == PF_NOISE_DEVICE) {
-    double n[PER];
-    normals_range<PER>(p.seed, i * NX + q * PER, p.epoch, STREAM_PROCESS, n);
+    const double* n = nrm;
     if (p.q_diag) {
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
@@ -1315,6 +1318,12 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
   double* H8 = sm + SM::H8;
   const double psi = Pm[L::AC], d0 = Pm[L::AC + 1];
   const double dlam = p.dlam;
+  // lane k < NZ: sensor k's position, R_kk^{-1/2}, R_kk^{-1} (this kernel runs for a diagonal R only) and
+  // z_k, loaded once instead of per pseudo-time step
+  const int kz = t < NZ ? t : 0;
+  const double sxk = Pm[L::AC + 2 + kz], syk = Pm[L::AC + 2 + NZ + kz];
+  const double rsk = t < NZ ? 1.0 / sqrt(Pm[L::R + kz * NZ + kz]) : 0.0;
+  const double rik = Pm[L::RI + kz * NZ + kz], zk = p.z[kz];
   // out[d] = (G v_pos)[d] = sum_b G[d][b] v[pos(b)]
   auto apply_G = [&](const double* v, double* out) {
     for (int d = t; d < NX; d += 64) {
@@ -1359,38 +1368,35 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
     for (int j = 0; j < p.L; ++j) {
       const double lam = p.lams[j];
       // ---- H8 = dh/d(positions) and h at eta (ledh.py:143-145; obs_jac_block's expressions) ----
-      for (int k = t; k < NZ; k += 64) {
-        const double sx = Pm[L::AC + 2 + k], sy = Pm[L::AC + 2 + NZ + k];
+      // lane k < NZ: row k of H8, h_k(eta), and R^{-1}(z - e) with e = h(eta) - H eta (diagonal R)
+      double h8[NR];
+      if (t < NZ) {
         double acc = 0.0;
 #pragma unroll
         for (int c = 0; c < NT; ++c) {
-          const double dx = eta[4 * c] - sx, dy = eta[4 * c + 1] - sy;
+          const double dx = eta[4 * c] - sxk, dy = eta[4 * c + 1] - syk;
           const double den = (dx * dx + dy * dy) + d0;
           acc += psi / den;
           const double den2 = den * den;
-          H8[k * NR + 2 * c] = (-2.0 * psi * dx) / den2;
-          H8[k * NR + 2 * c + 1] = (-2.0 * psi * dy) / den2;
+          h8[2 * c] = (-2.0 * psi * dx) / den2;
+          h8[2 * c + 1] = (-2.0 * psi * dy) / den2;
         }
-        sm[SM::HV + k] = acc;
+        sm[SM::HV + t] = acc;
         double he = 0.0;  // H eta over the nonzero columns, in column order
 #pragma unroll
-        for (int a = 0; a < NR; ++a) he += H8[k * NR + a] * eta[lr_pos(a)];
-        sm[SM::ZE + k] = acc - he;  // e = h(eta) - H eta
-      }
-      __syncthreads();
-      // ---- R^{-1}(z - e), r8 = H8^T R^{-1}(z - e) --------------------------------
-      for (int k = t; k < NZ; k += 64) {
-        double acc = 0.0;
-        for (int l = 0; l < NZ; ++l) acc += Pm[L::RI + k * NZ + l] * (p.z[l] - sm[SM::ZE + l]);
-        sm[SM::RU + k] = acc;
+        for (int a = 0; a < NR; ++a) {
+          H8[t * NR + a] = h8[a];
+          he += h8[a] * eta[lr_pos(a)];
+        }
+        sm[SM::RU + t] = rik * (zk - (acc - he));
+      } else {
+#pragma unroll
+        for (int a = 0; a < NR; ++a) h8[a] = 0.0;
       }
       // ---- Householder QR of U = R^{-1/2} H8 over the wave: lane k holds row k (NZ <= 64) -------
       double u[NR];
-      {
-        const double rs = t < NZ ? 1.0 / sqrt(Pm[L::R + t * NZ + t]) : 0.0;
 #pragma unroll
-        for (int a = 0; a < NR; ++a) u[a] = t < NZ ? H8[t * NR + a] * rs : 0.0;
-      }
+      for (int a = 0; a < NR; ++a) u[a] = h8[a] * rsk;
 #pragma unroll
       for (int pc = 0; pc < NR; ++pc) {
         const double xk = t >= pc ? u[pc] : 0.0;
