@@ -1145,4 +1145,14 @@ int32_t pf_ledh_shared_path(pf_ledh_handle* h) { return (h && h->shared) ? 1 : 0
 extern "C" int pf_debug_stamps_ledh(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pf::ledh::g_ledh_stamps), (size_t)n * sizeof(unsigned long long));
 }
+// k_flow_wave_lr phase accumulators (workgroup 0): read (n <= 16) and clear
+extern "C" int pf_debug_lr_acc(unsigned long long* out, int n, int clear) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf::ledh::g_lr_acc), (size_t)n * sizeof(unsigned long long)) != hipSuccess)
+    return 1;
+  if (clear) {
+    static const unsigned long long zeros[16] = {};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pf::ledh::g_lr_acc), zeros, sizeof(zeros));
+  }
+  return 0;
+}
 #endif

@@ -220,10 +220,10 @@ __global__ void __launch_bounds__(ekf_block<NZ>()) k_ekf_seq(const double* __res
 #pragma unroll
       for (int r = 0; r < NZ; ++r)
         col[r] = lane < NZ ? SA[r * NZ + lane] : (lane < NZ + NX ? PHT[(lane - NZ) * NZ + r] : 0.0);
-      double ld;
+      DetAcc det;
       int sg;
-      lr_gauss_jordan<NZ>(col, &ld, &sg);
-      (void)ld;
+      lr_gauss_jordan<NZ>(col, &det, &sg);
+      (void)det;
       (void)sg;
       if (lane >= NZ && lane < NZ + NX) {  // row d of K = P H^T S^{-1}; x += K (z - h(x))
         const int d = lane - NZ;

@@ -55,9 +55,22 @@ __device__ unsigned long long g_ledh_stamps[256 * FST];
   do {                                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < 256) g_ledh_stamps[blockIdx.x * FST + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// k_flow_wave_lr phase accumulators (workgroup 0, thread 0): ticks of 10 ns per phase over a launch
+__device__ unsigned long long g_lr_acc[16];
+#define LR_MARK(k)                                                          \
+  do {                                                                      \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                              \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
+      g_lr_acc[k] += now_ - lr_last_;                                       \
+      lr_last_ = now_;                                                      \
+    }                                                                       \
+  } while (0)
 #else
 #define LF_STAMP(k) \
   do {              \
+  } while (0)
+#define LR_MARK(k) \
+  do {             \
   } while (0)
 #endif
 
@@ -1212,11 +1225,27 @@ struct LrSmem {
 // state index of position component a (x, y of target a / 2)
 __device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
 
+// |det| as mantissa x 2^exponent: the pivots' product renormalised after every factor (no overflow, and
+// one log per determinant - or per ratio of two - instead of one per pivot)
+struct DetAcc {
+  double m = 1.0;
+  int e = 0;
+  __device__ __forceinline__ void mul(double a) {
+    int k;
+    m = frexp(m * a, &k);
+    e += k;
+  }
+};
+// log(|det A| / |det B|)
+__device__ __forceinline__ double det_log_ratio(const DetAcc& a, const DetAcc& b) {
+  return log(a.m / b.m) + (double)(a.e - b.e) * 0.69314718055994530942;
+}
+
 // Gauss-Jordan with partial pivoting on the NR x 2NR matrix [B | I] held column per lane (lane c < 2NR:
-// col[r] = row r of column c): -> [I | B^{-1}] (lanes NR .. 2NR - 1), log|det B|, sign.  One wave.
+// col[r] = row r of column c): -> [I | B^{-1}] (lanes NR .. 2NR - 1), |det B|, sign.  One wave.
 template <int NR>
-__device__ __forceinline__ void lr_gauss_jordan(double (&col)[NR], double* logabs, int* sign) {
-  double la = 0.0;
+__device__ __forceinline__ void lr_gauss_jordan(double (&col)[NR], DetAcc* det, int* sign) {
+  DetAcc dacc;
   int sg = 1;
 #pragma unroll
   for (int p = 0; p < NR; ++p) {
@@ -1242,7 +1271,7 @@ __device__ __forceinline__ void lr_gauss_jordan(double (&col)[NR], double* logab
         f[r] = fa;
       }
     const double piv = f[p];
-    la += log(fabs(piv));
+    dacc.mul(fabs(piv));
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
     const double bp = col[p] / piv;
@@ -1251,15 +1280,15 @@ __device__ __forceinline__ void lr_gauss_jordan(double (&col)[NR], double* logab
     for (int r = 0; r < NR; ++r)
       if (r != p) col[r] = col[r] - f[r] * bp;
   }
-  *logabs = la;
+  *det = dacc;
   *sign = sg;
 }
 
-// log|det T| and its sign by LU with partial pivoting, T NR x NR column per lane (lanes c < NR)
+// |det T| and its sign by LU with partial pivoting, T NR x NR column per lane (lanes c < NR)
 template <int NR>
-__device__ __forceinline__ void lr_logdet(double (&col)[NR], double* logabs, int* sign) {
+__device__ __forceinline__ void lr_logdet(double (&col)[NR], DetAcc* det, int* sign) {
   const int c = threadIdx.x & 63;
-  double la = 0.0;
+  DetAcc dacc;
   int sg = 1;
 #pragma unroll
   for (int p = 0; p < NR; ++p) {
@@ -1285,7 +1314,7 @@ __device__ __forceinline__ void lr_logdet(double (&col)[NR], double* logabs, int
         f[r] = fa;
       }
     const double piv = f[p];
-    la += log(fabs(piv));
+    dacc.mul(fabs(piv));
     if (piv < 0.0) sg = -sg;
     if (piv == 0.0) sg = 0;
     if (c > p) {
@@ -1294,7 +1323,41 @@ __device__ __forceinline__ void lr_logdet(double (&col)[NR], double* logabs, int
       for (int r = p + 1; r < NR; ++r) col[r] = col[r] - f[r] * bp;
     }
   }
-  *logabs = la;
+  *det = dacc;
+  *sign = sg;
+}
+
+// Gauss-Jordan on [D | B | C] without pivoting, column per lane (lanes 0..NR-1: D, NR..2NR-1: B,
+// 2NR..3NR-1: C; D and C symmetric positive definite with eigenvalues >= 1, so no pivot is small):
+// lanes NR..2NR-1 end with D^{-1} B, and |det D|, |det C| come from the pivots.  The two
+// eliminations share one instruction stream (the C lanes eliminate with C's pivot column), instead of
+// a pivoted Gauss-Jordan and a pivoted LU one after the other.
+template <int NR>
+__device__ __forceinline__ void lr_gj_pair(double (&col)[NR], DetAcc* detD, DetAcc* detC, int* sign) {
+  const int lane = threadIdx.x & 63;
+  const bool cl = lane >= 2 * NR;
+  DetAcc dd, dc;
+  int sg = 1;
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    double f[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double fd = readlane_d(col[r], p), fc = readlane_d(col[r], 2 * NR + p);
+      f[r] = cl ? fc : fd;
+    }
+    const double pd = readlane_d(col[p], p), pcv = readlane_d(col[p], 2 * NR + p);
+    dd.mul(fabs(pd));
+    dc.mul(fabs(pcv));
+    if (!(pd > 0.0) || !(pcv > 0.0)) sg = 0;  // not positive definite after all (NaN, ...)
+    const double bp = col[p] / f[p];
+    col[p] = bp;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r != p) col[r] = col[r] - f[r] * bp;
+  }
+  *detD = dd;
+  *detC = dc;
   *sign = sg;
 }
 
@@ -1334,6 +1397,9 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
     }
     __syncthreads();
   };
+#ifdef PF_STAMPS
+  unsigned long long lr_last_ = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int64_t i = blockIdx.x; i < p.N; i += gridDim.x) {
     // ---- eta0 = g(x_{k-1}, u) + v (as k_flow_wave) ----------------------------
     for (int d = t; d < NX; d += 64) sm[SM::XP + d] = p.x_in[(int64_t)d * p.Npad + i];
@@ -1364,6 +1430,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       eta[d] = e0;
     }
     __syncthreads();
+    LR_MARK(7);
     double theta = 0.0;
     for (int j = 0; j < p.L; ++j) {
       const double lam = p.lams[j];
@@ -1393,23 +1460,31 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
         for (int a = 0; a < NR; ++a) h8[a] = 0.0;
       }
+      LR_MARK(0);
       // ---- Householder QR of U = R^{-1/2} H8 over the wave: lane k holds row k (NZ <= 64) -------
       double u[NR];
 #pragma unroll
       for (int a = 0; a < NR; ++a) u[a] = h8[a] * rsk;
+      // Reflector pc: v = x - alpha e_pc (x = column pc's rows >= pc, alpha = -sign(x_pc) |x|).  Every
+      // reduction of the step is issued at once - |x|^2 and x^T u_c of the trailing columns - since
+      // v^T v = 2 alpha (alpha - x_pc) and v^T u_c = x^T u_c - alpha u_{pc,c} (LAPACK's dlarfg / dlarf
+      // algebra): one wave-sum level per column instead of three
 #pragma unroll
       for (int pc = 0; pc < NR; ++pc) {
         const double xk = t >= pc ? u[pc] : 0.0;
+        double dot[NR];
         const double nrm2 = wave_sum_ud(xk * xk);
+#pragma unroll
+        for (int c = pc + 1; c < NR; ++c) dot[c] = wave_sum_ud(xk * u[c]);
         const double xp = readlane_d(u[pc], pc);
         const double alpha = xp >= 0.0 ? -sqrt(nrm2) : sqrt(nrm2);
         const double vk = t == pc ? xp - alpha : xk;  // the reflector v (rows >= pc)
-        const double vtv = wave_sum_ud(vk * vk);
+        const double vtv = 2.0 * alpha * (alpha - xp);
         if (vtv > 0.0) {
           const double beta = 2.0 / vtv;
 #pragma unroll
           for (int c = pc + 1; c < NR; ++c) {
-            const double sc = wave_sum_ud(vk * u[c]);
+            const double sc = dot[c] - alpha * readlane_d(u[c], pc);
             u[c] = u[c] - beta * vk * sc;
           }
         }
@@ -1419,6 +1494,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
         for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
       __syncthreads();
+      LR_MARK(1);
       for (int a = t; a < NR; a += 64) {
         double acc = 0.0;
         for (int k = 0; k < NZ; ++k) acc += H8[k * NR + a] * sm[SM::RU + k];
@@ -1448,44 +1524,64 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         }
       }
       __syncthreads();
+      LR_MARK(2);
       // ---- D = I + lam Rq P_pp Rq^T, D1 = I + c1 (..), column per lane: [D | Rq] -> [I | D^{-1} Rq] ----
       const double c1 = lam - 0.5 * dlam;
-      double m2[NR];  // column (t mod NR) of Rq P_pp Rq^T (lanes < NR), or of Rq (lanes NR .. 2NR - 1)
+      // column (t mod NR) of M = Rq P_pp Rq^T (lanes < NR and 2NR .. 3NR - 1), or of Rq (lanes NR .. 2NR - 1)
+      double m2[NR];
+      const bool in_b = t >= NR && t < 2 * NR, in_c = t >= 2 * NR && t < 3 * NR;
       {
-        const int cc = t < NR ? t : (t < 2 * NR ? t - NR : 0);
+        const int cc = t < NR ? t : (in_b ? t - NR : (in_c ? t - 2 * NR : 0));
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           double acc = 0.0;
 #pragma unroll
           for (int m = 0; m < NR; ++m) acc += sm[SM::TT + r * NR + m] * sm[SM::RQ + cc * NR + m];
-          m2[r] = t < NR ? acc : sm[SM::RQ + r * NR + cc];
+          m2[r] = in_b ? sm[SM::RQ + r * NR + cc] : acc;
         }
       }
-      double colD[NR], colC[NR];
+      // [D | Rq | C], D = I + lam M, C = I + c1 M (det(I + dlam A) = det C / det D)
+      double colD[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        const double id = (t < NR && r == t) ? 1.0 : 0.0;
-        colD[r] = t < NR ? id + lam * m2[r] : m2[r];  // [D | Rq]
-        colC[r] = id + c1 * m2[r];
+        if (t < NR) colD[r] = (r == t ? 1.0 : 0.0) + lam * m2[r];
+        else if (in_b) colD[r] = m2[r];
+        else if (in_c) colD[r] = (r == t - 2 * NR ? 1.0 : 0.0) + c1 * m2[r];
+        else colD[r] = 0.0;
       }
-      double D_ld, C_ld;
-      int D_sg, C_sg;
-      lr_gauss_jordan<NR>(colD, &D_ld, &D_sg);
-      lr_logdet<NR>(colC, &C_ld, &C_sg);
-      if (C_sg * D_sg > 0) {
-        theta += C_ld - D_ld;
+      DetAcc D_d, C_d;
+      int DC_sg;
+      lr_gj_pair<NR>(colD, &D_d, &C_d, &DC_sg);
+      if (DC_sg > 0) {
+        theta += det_log_ratio(C_d, D_d);
       } else {  // the reference's +1e-12 I retry (ledh.py:174-179), as flow_logdet
-        const double eps = 1e-12;
-        const double c2 = lam - dlam / (2.0 * (1.0 + eps));
+        double colC[NR];
+        int C_sg, D_sg = 1;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) colC[r] = ((t < NR && r == t) ? 1.0 : 0.0) + c2 * m2[r];
-        lr_logdet<NR>(colC, &C_ld, &C_sg);
-        theta += (double)NX * log1p(eps) + C_ld - D_ld;
+        for (int r = 0; r < NR; ++r) colC[r] = ((t < NR && r == t) ? 1.0 : 0.0) + c1 * m2[r];
+        lr_logdet<NR>(colC, &C_d, &C_sg);
+        {
+          double colE[NR];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) colE[r] = ((t < NR && r == t) ? 1.0 : 0.0) + lam * m2[r];
+          lr_logdet<NR>(colE, &D_d, &D_sg);
+        }
+        if (C_sg * D_sg > 0) {
+          theta += det_log_ratio(C_d, D_d);
+        } else {
+          const double eps = 1e-12;
+          const double c2 = lam - dlam / (2.0 * (1.0 + eps));
+#pragma unroll
+          for (int r = 0; r < NR; ++r) colC[r] = ((t < NR && r == t) ? 1.0 : 0.0) + c2 * m2[r];
+          lr_logdet<NR>(colC, &C_d, &C_sg);
+          theta += (double)NX * log1p(eps) + det_log_ratio(C_d, D_d);
+        }
       }
       if (t >= NR && t < 2 * NR)
 #pragma unroll
         for (int r = 0; r < NR; ++r) sm[SM::X + r * NR + (t - NR)] = colD[r];  // D^{-1} Rq
       __syncthreads();
+      LR_MARK(3);
       // ---- Y = Rq^T D^{-1} Rq;  c = P_{:,pos} r8 ---------------------------------
       for (int q = t; q < NR * NR; q += 64) {
         const int a = q / NR, b = q - a * NR;
@@ -1501,6 +1597,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         cv[d] = acc;
       }
       __syncthreads();
+      LR_MARK(4);
       // ---- G = -1/2 P_{:,pos} Y ------------------------------------------------
       for (int q = t; q < NX * NR; q += 64) {
         const int d = q / NR, b = q - d * NR;
@@ -1510,6 +1607,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         sm[SM::G + q] = -0.5 * acc;
       }
       __syncthreads();
+      LR_MARK(5);
       // ---- b = (I + 2 lam A)[(I + lam A) c + A eta0], eta += dlam (A eta + b)  (ledh.py:165-171) ----
       apply_G(eta0, t1);  // t1 = A eta0
       apply_G(cv, t2);    // t2 = A c
@@ -1521,6 +1619,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       apply_G(eta, t2);   // t2 = A eta
       for (int d = t; d < NX; d += 64) eta[d] = eta[d] + dlam * (t2[d] + t1[d]);
       __syncthreads();
+      LR_MARK(6);
     }
     // ---- weight (ledh.py:186-190), as k_flow_wave ---------------------------------
     for (int k = t; k < NZ; k += 64) {
@@ -1553,6 +1652,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
     if (t == 0) p.lw[i] = (log(p.w_in[i] + 1e-300) + theta) + tot;
     for (int d = t; d < NX; d += 64) p.x_out[(int64_t)d * p.Npad + i] = eta[d];
     __syncthreads();
+    LR_MARK(8);
   }
 }
 

@@ -52,18 +52,22 @@ def jac(eta, mpm=False):
 
 
 def householder_r(U):
+    """The kernel's Householder QR (k_flow_wave_lr): per reflector all reductions at once,
+    v^T v = 2 alpha (alpha - x_p), v^T u_c = x^T u_c - alpha u_{p,c}."""
     U = U.copy()
     m = U.shape[1]
     for p in range(m):
         x = U[p:, p].copy()
         nrm2, xp = np.sum(x * x), x[0]
+        dots = {c: np.sum(x * U[p:, c]) for c in range(p + 1, m)}
         alpha = -np.sqrt(nrm2) if xp >= 0 else np.sqrt(nrm2)
         v = x.copy()
         v[0] = xp - alpha
-        vtv = np.sum(v * v)
+        vtv = 2.0 * alpha * (alpha - xp)
         if vtv > 0:
             for c in range(p + 1, m):
-                U[p:, c] -= (2.0 / vtv) * v * np.sum(v * U[p:, c])
+                sc = dots[c] - alpha * U[p, c]
+                U[p:, c] -= (2.0 / vtv) * v * sc
         U[p, p], U[p + 1:, p] = alpha, 0.0
     return U[:m]
 
