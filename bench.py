@@ -368,14 +368,16 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
         data_desc = ("synthetic (simulate_acoustic_dataset 4 targets 5x5 sensors psi=10 d0=0.1 seed=56 article init; "
                      "R=0.01 I, Q=blockdiag(article_process_noise_cov))")
         notes = (f"N={Np} particles, {L} lambda steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
-                 "(analytic acoustic Jacobian), per-particle LEDH flow (pf_ledh_kernels.h k_flow_wave), Philox noise")
+                 "(analytic acoustic Jacobian), per-particle LEDH flow in the targets' position space "
+                 "(pf_ledh_kernels.h k_flow_wave_lr), Philox noise")
     else:
         wl_name = "L96 d=40"
         data_desc = "synthetic (simulate_lorenz96 nx=40 spinup=1000 obs_interval=1 obs_fraction=4 seed=42)"
         notes = ("N=1e4 particles, 8 lambda steps, ESS-ratio 0.5 systematic resampling, EKF tracker on the device "
                  "(analytic RK4 Jacobian), Philox process noise")
-    ltraffic = pmc_traffic("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
-                           "k_flow_wave" if per_particle else "k_ledh_fused")[0]
+    # the per-particle flow kernel: the position-space one for the acoustic h with diagonal R
+    flow_kernel = ("k_flow_wave_lr" if model == "mat" else "k_flow_wave") if per_particle else "k_ledh_fused"
+    ltraffic = pmc_traffic("ledh_mat" if (model == "mat" and algo == "ledh") else algo, flow_kernel)[0]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -428,7 +430,7 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
                          "traffic_frac": None if ltraffic is None else ltraffic / (dev_s / K) / 1e9 / HBM_PEAK_GBS,
                          "traffic_unit": "HBM bytes per filter step of the kernel (rocprofv3 FETCH_SIZE x2 + "
                                          "WRITE_SIZE, profiles/pmc_traffic_<workload>.json)",
-                         "kernel": ("whole LEDH job: k_ekf_seq + " + ("per step k_flow_wave (per-particle flow)"
+                         "kernel": ("whole LEDH job: k_ekf_seq + " + (f"per step {flow_kernel} (per-particle flow)"
                                                                       if per_particle else
                                                                       "k_setup/k_compose + per step k_ledh_fused"))
                                    if algo == "ledh" else "whole EDH job: k_ekf_seq + k_edh_setup + per step k_ledh_fused",
@@ -436,7 +438,7 @@ def main_ledh(args, world, rank, local, algo="ledh", use_dist=False, model="l96"
                          "flops_note": "the reference formulation's per-particle dense algebra (estimate)"
                                        if per_particle else "shared-Jacobian flow (see ledh_flops_per_particle)",
                          "valu": pmc_valu("ledh_mat" if (model == "mat" and algo == "ledh") else algo,
-                                          "k_flow_wave" if per_particle else "k_ledh_fused", dev_s * 1e6 / K)},
+                                          flow_kernel, dev_s * 1e6 / K)},
             "cpu_baseline": cpu,
         }
         if model == "mat" and algo == "ledh":

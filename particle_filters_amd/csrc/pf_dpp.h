@@ -26,6 +26,15 @@ __device__ __forceinline__ double dpp_d(double old, double v) {
   const int hi = dpp_i<CTRL, RM>((int)(o >> 32), (int)(x >> 32));
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+// the same move where every lane's source is valid (quad_perm, row mirrors, row_newbcast; or rows
+// outside RM whose result is not read): no initialising move of the destination's old value
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ double dpp_mov_d(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)x, CTRL, RM, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, RM, 0xf, true);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 enum : int {
   DPP_QP_1032 = 0xB1,
   DPP_QP_2301 = 0x4E,

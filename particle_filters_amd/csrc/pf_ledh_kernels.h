@@ -1225,6 +1225,59 @@ struct LrSmem {
 // state index of position component a (x, y of target a / 2)
 __device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
 
+// sums over the lanes of the sensor rows of N values at once, level by level (each DPP move reads a
+// register written N instructions earlier: no DPP hazard stalls): the lower 32 lanes when NZ <= 32
+// (one level less than a wave sum; the upper lanes hold zeros), the whole wave otherwise.  Every lane
+// ends with the sums.
+template <int NZ, int N>
+__device__ __forceinline__ void lr_row_sums(double (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_QP_1032>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_QP_2301>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_HMIRROR>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_MIRROR>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_BCAST15, 0xa>(v[i]);  // rows 0, 2 not read
+  if constexpr (NZ > 32) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_BCAST31, 0xc>(v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = readlane_d(v[i], NZ > 32 ? 63 : 31);
+}
+
+// Householder reflector PC of the QR of U over the wave (lane k holds row k): v = x - alpha e_PC
+// (x = column PC's rows >= PC, alpha = -sign(x_PC) |x|).  Every reduction of the step is issued at
+// once - |x|^2 and x^T u_c of the trailing columns - since v^T v = 2 alpha (alpha - x_PC) and
+// v^T u_c = x^T u_c - alpha u_{PC,c} (LAPACK's dlarfg / dlarf algebra): one wave-sum level per column.
+template <int NR, int NZ, int PC>
+__device__ __forceinline__ void lr_qr_col(double (&u)[NR], int t) {
+  constexpr int N = NR - PC;  // |x|^2, then x^T u_c for c > PC
+  const double xk = t >= PC ? u[PC] : 0.0;
+  double sv[N];
+  sv[0] = xk * xk;
+#pragma unroll
+  for (int c = PC + 1; c < NR; ++c) sv[c - PC] = xk * u[c];
+  lr_row_sums<NZ, N>(sv);
+  const double xp = readlane_d(u[PC], PC);
+  const double alpha = xp >= 0.0 ? -sqrt(sv[0]) : sqrt(sv[0]);
+  const double vk = t == PC ? xp - alpha : xk;  // the reflector v (rows >= PC)
+  const double vtv = 2.0 * alpha * (alpha - xp);
+  if (vtv > 0.0) {
+    const double beta = 2.0 / vtv;
+#pragma unroll
+    for (int c = PC + 1; c < NR; ++c) {
+      const double sc = sv[c - PC] - alpha * readlane_d(u[c], PC);
+      u[c] = u[c] - beta * vk * sc;
+    }
+  }
+  u[PC] = t == PC ? alpha : (t > PC ? 0.0 : u[PC]);
+  if constexpr (PC + 1 < NR) lr_qr_col<NR, NZ, PC + 1>(u, t);
+}
+
 // |det| as mantissa x 2^exponent: the pivots' product renormalised after every factor (no overflow, and
 // one log per determinant - or per ratio of two - instead of one per pivot)
 struct DetAcc {
@@ -1327,38 +1380,39 @@ __device__ __forceinline__ void lr_logdet(double (&col)[NR], DetAcc* det, int* s
   *sign = sg;
 }
 
-// Gauss-Jordan on [D | B | C] without pivoting, column per lane (lanes 0..NR-1: D, NR..2NR-1: B,
-// 2NR..3NR-1: C; D and C symmetric positive definite with eigenvalues >= 1, so no pivot is small):
-// lanes NR..2NR-1 end with D^{-1} B, and |det D|, |det C| come from the pivots.  The two
-// eliminations share one instruction stream (the C lanes eliminate with C's pivot column), instead of
-// a pivoted Gauss-Jordan and a pivoted LU one after the other.
+// Gauss-Jordan on [D | B | C] without pivoting, column per lane: D in lanes 0..NR-1 and B in NR..2NR-1
+// (row 0 of the wave), C in lanes LR_CB..LR_CB+NR-1 (row 1); D and C symmetric positive definite with
+// eigenvalues >= 1, so no pivot is small.  Lanes NR..2NR-1 end with D^{-1} B, and |det D|, |det C| come
+// from the pivots.  Each 16-lane row takes its pivot column with DPP row_newbcast (one v_mov_dpp per
+// dword, no scalar round trip), so the two eliminations share one instruction stream: row 0
+// eliminates with D's pivot column, row 1 with C's.
+constexpr int LR_CB = 16;
+template <int NR, int P>
+__device__ __forceinline__ void lr_gj_pivot(double (&col)[NR], DetAcc& det, bool& ok) {
+  double f[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) f[r] = dpp_mov_d<0x150 + P>(col[r]);  // row_newbcast: lane P of this row
+  det.mul(fabs(f[P]));
+  ok = ok && (f[P] > 0.0);  // not positive definite after all (NaN, ...)
+  const double bp = col[P] / f[P];
+  col[P] = bp;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r != P) col[r] = col[r] - f[r] * bp;
+  if constexpr (P + 1 < NR) lr_gj_pivot<NR, P + 1>(col, det, ok);
+}
 template <int NR>
 __device__ __forceinline__ void lr_gj_pair(double (&col)[NR], DetAcc* detD, DetAcc* detC, int* sign) {
-  const int lane = threadIdx.x & 63;
-  const bool cl = lane >= 2 * NR;
-  DetAcc dd, dc;
-  int sg = 1;
-#pragma unroll
-  for (int p = 0; p < NR; ++p) {
-    double f[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const double fd = readlane_d(col[r], p), fc = readlane_d(col[r], 2 * NR + p);
-      f[r] = cl ? fc : fd;
-    }
-    const double pd = readlane_d(col[p], p), pcv = readlane_d(col[p], 2 * NR + p);
-    dd.mul(fabs(pd));
-    dc.mul(fabs(pcv));
-    if (!(pd > 0.0) || !(pcv > 0.0)) sg = 0;  // not positive definite after all (NaN, ...)
-    const double bp = col[p] / f[p];
-    col[p] = bp;
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-      if (r != p) col[r] = col[r] - f[r] * bp;
-  }
-  *detD = dd;
-  *detC = dc;
-  *sign = sg;
+  static_assert(2 * NR <= LR_CB, "D and B in one 16-lane row");
+  DetAcc det;  // this row's pivots: D's in row 0, C's in row 1
+  bool ok = true;
+  lr_gj_pivot<NR, 0>(col, det, ok);
+  detD->m = readlane_d(det.m, 0);
+  detD->e = __builtin_amdgcn_readlane(det.e, 0);
+  detC->m = readlane_d(det.m, LR_CB);
+  detC->e = __builtin_amdgcn_readlane(det.e, LR_CB);
+  const int okv = ok ? 1 : 0;
+  *sign = (__builtin_amdgcn_readlane(okv, 0) & __builtin_amdgcn_readlane(okv, LR_CB)) ? 1 : 0;
 }
 
 template <int NX, int NZ, int TK>
@@ -1377,7 +1431,6 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
   double* eta0 = sm + SM::E0;
   double* t1 = sm + SM::T1;
   double* t2 = sm + SM::T2;
-  double* cv = sm + SM::CV;
   double* H8 = sm + SM::H8;
   const double psi = Pm[L::AC], d0 = Pm[L::AC + 1];
   const double dlam = p.dlam;
@@ -1387,16 +1440,17 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
   const double sxk = Pm[L::AC + 2 + kz], syk = Pm[L::AC + 2 + NZ + kz];
   const double rsk = t < NZ ? 1.0 / sqrt(Pm[L::R + kz * NZ + kz]) : 0.0;
   const double rik = Pm[L::RI + kz * NZ + kz], zk = p.z[kz];
-  // out[d] = (G v_pos)[d] = sum_b G[d][b] v[pos(b)]
-  auto apply_G = [&](const double* v, double* out) {
-    for (int d = t; d < NX; d += 64) {
-      double acc = 0.0;
+  // lane NR + a: row a of P_pp; lane d < NX: row d of P_{:,pos} (the flow update's operands)
+  const bool in_b = t >= NR && t < 2 * NR, in_c = t >= LR_CB && t < LR_CB + NR;
+  double pp[NR], prow[NR];
+  {
+    const int a = in_b ? t - NR : 0, d = t < NX ? t : 0;
 #pragma unroll
-      for (int b = 0; b < NR; ++b) acc += sm[SM::G + d * NR + b] * v[lr_pos(b)];
-      out[d] = acc;
+    for (int b = 0; b < NR; ++b) {
+      pp[b] = P[lr_pos(a) * NX + lr_pos(b)];
+      prow[b] = P[d * NX + lr_pos(b)];
     }
-    __syncthreads();
-  };
+  }
 #ifdef PF_STAMPS
   unsigned long long lr_last_ = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1430,18 +1484,25 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       eta[d] = e0;
     }
     __syncthreads();
+    double e0p[NR];  // eta0's position components (uniform)
+#pragma unroll
+    for (int a = 0; a < NR; ++a) e0p[a] = eta0[lr_pos(a)];
     LR_MARK(7);
     double theta = 0.0;
     for (int j = 0; j < p.L; ++j) {
       const double lam = p.lams[j];
+      double etap[NR];  // eta's position components (uniform)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) etap[a] = eta[lr_pos(a)];
       // ---- H8 = dh/d(positions) and h at eta (ledh.py:143-145; obs_jac_block's expressions) ----
       // lane k < NZ: row k of H8, h_k(eta), and R^{-1}(z - e) with e = h(eta) - H eta (diagonal R)
       double h8[NR];
+      double ru = 0.0;
       if (t < NZ) {
         double acc = 0.0;
 #pragma unroll
         for (int c = 0; c < NT; ++c) {
-          const double dx = eta[4 * c] - sxk, dy = eta[4 * c + 1] - syk;
+          const double dx = etap[2 * c] - sxk, dy = etap[2 * c + 1] - syk;
           const double den = (dx * dx + dy * dy) + d0;
           acc += psi / den;
           const double den2 = den * den;
@@ -1453,53 +1514,29 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
         for (int a = 0; a < NR; ++a) {
           H8[t * NR + a] = h8[a];
-          he += h8[a] * eta[lr_pos(a)];
+          he += h8[a] * etap[a];
         }
-        sm[SM::RU + t] = rik * (zk - (acc - he));
+        ru = rik * (zk - (acc - he));
       } else {
 #pragma unroll
         for (int a = 0; a < NR; ++a) h8[a] = 0.0;
       }
       LR_MARK(0);
+      // r8 = H8^T R^{-1}(z - e) (uniform), its wave sums issued with the QR's first column
+      double r8[NR];
+#pragma unroll
+      for (int a = 0; a < NR; ++a) r8[a] = h8[a] * ru;
+      lr_row_sums<NZ, NR>(r8);
       // ---- Householder QR of U = R^{-1/2} H8 over the wave: lane k holds row k (NZ <= 64) -------
       double u[NR];
 #pragma unroll
       for (int a = 0; a < NR; ++a) u[a] = h8[a] * rsk;
-      // Reflector pc: v = x - alpha e_pc (x = column pc's rows >= pc, alpha = -sign(x_pc) |x|).  Every
-      // reduction of the step is issued at once - |x|^2 and x^T u_c of the trailing columns - since
-      // v^T v = 2 alpha (alpha - x_pc) and v^T u_c = x^T u_c - alpha u_{pc,c} (LAPACK's dlarfg / dlarf
-      // algebra): one wave-sum level per column instead of three
-#pragma unroll
-      for (int pc = 0; pc < NR; ++pc) {
-        const double xk = t >= pc ? u[pc] : 0.0;
-        double dot[NR];
-        const double nrm2 = wave_sum_ud(xk * xk);
-#pragma unroll
-        for (int c = pc + 1; c < NR; ++c) dot[c] = wave_sum_ud(xk * u[c]);
-        const double xp = readlane_d(u[pc], pc);
-        const double alpha = xp >= 0.0 ? -sqrt(nrm2) : sqrt(nrm2);
-        const double vk = t == pc ? xp - alpha : xk;  // the reflector v (rows >= pc)
-        const double vtv = 2.0 * alpha * (alpha - xp);
-        if (vtv > 0.0) {
-          const double beta = 2.0 / vtv;
-#pragma unroll
-          for (int c = pc + 1; c < NR; ++c) {
-            const double sc = dot[c] - alpha * readlane_d(u[c], pc);
-            u[c] = u[c] - beta * vk * sc;
-          }
-        }
-        u[pc] = t == pc ? alpha : (t > pc ? 0.0 : u[pc]);
-      }
+      lr_qr_col<NR, NZ, 0>(u, t);
       if (t < NR)
 #pragma unroll
         for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
       __syncthreads();
       LR_MARK(1);
-      for (int a = t; a < NR; a += 64) {
-        double acc = 0.0;
-        for (int k = 0; k < NZ; ++k) acc += H8[k * NR + a] * sm[SM::RU + k];
-        sm[SM::R8 + a] = acc;
-      }
       // TT = Rq P_pp
       for (int q = t; q < NR * NR; q += 64) {
         const int r = q / NR, m = q - r * NR;
@@ -1527,11 +1564,10 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       LR_MARK(2);
       // ---- D = I + lam Rq P_pp Rq^T, D1 = I + c1 (..), column per lane: [D | Rq] -> [I | D^{-1} Rq] ----
       const double c1 = lam - 0.5 * dlam;
-      // column (t mod NR) of M = Rq P_pp Rq^T (lanes < NR and 2NR .. 3NR - 1), or of Rq (lanes NR .. 2NR - 1)
+      // column cc of M = Rq P_pp Rq^T (lanes < NR and LR_CB .. LR_CB + NR - 1), or of Rq (lanes NR .. 2NR - 1)
       double m2[NR];
-      const bool in_b = t >= NR && t < 2 * NR, in_c = t >= 2 * NR && t < 3 * NR;
       {
-        const int cc = t < NR ? t : (in_b ? t - NR : (in_c ? t - 2 * NR : 0));
+        const int cc = t < NR ? t : (in_b ? t - NR : (in_c ? t - LR_CB : 0));
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           double acc = 0.0;
@@ -1542,13 +1578,13 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       }
       // [D | Rq | C], D = I + lam M, C = I + c1 M (det(I + dlam A) = det C / det D)
       double colD[NR];
+      {
+        const double sc = t < NR ? lam : (in_b ? 1.0 : (in_c ? c1 : 0.0));
+        const int dr = t < NR ? t : (in_c ? t - LR_CB : -1);
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (t < NR) colD[r] = (r == t ? 1.0 : 0.0) + lam * m2[r];
-        else if (in_b) colD[r] = m2[r];
-        else if (in_c) colD[r] = (r == t - 2 * NR ? 1.0 : 0.0) + c1 * m2[r];
-        else colD[r] = 0.0;
+        for (int r = 0; r < NR; ++r) colD[r] = (r == dr ? 1.0 : 0.0) + sc * m2[r];
       }
+      LR_MARK(9);
       DetAcc D_d, C_d;
       int DC_sg;
       lr_gj_pair<NR>(colD, &D_d, &C_d, &DC_sg);
@@ -1577,47 +1613,53 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
           theta += (double)NX * log1p(eps) + det_log_ratio(C_d, D_d);
         }
       }
-      if (t >= NR && t < 2 * NR)
+      if (in_b)
 #pragma unroll
         for (int r = 0; r < NR; ++r) sm[SM::X + r * NR + (t - NR)] = colD[r];  // D^{-1} Rq
       __syncthreads();
       LR_MARK(3);
-      // ---- Y = Rq^T D^{-1} Rq;  c = P_{:,pos} r8 ---------------------------------
-      for (int q = t; q < NR * NR; q += 64) {
-        const int a = q / NR, b = q - a * NR;
-        double acc = 0.0;
+      // ---- the flow update in the position space (ledh.py:165-171) ------------------------------
+      // A v = P_{:,pos} K v_pos with K = -1/2 Rq^T D^{-1} Rq (8 x 8) and c = P_{:,pos} r8, so
+      //   w = c + lam A c + A eta0 = P_{:,pos} om,        om = r8 + K (lam P_pp r8 + eta0_pos)
+      //   b = (I + 2 lam A) w     = P_{:,pos} (om + 2 lam K P_pp om)
+      //   eta += dlam (A eta + b) = eta + dlam P_{:,pos} (om + 2 lam K P_pp om + K eta_pos)
+      // lane NR + a holds row a of K and of P_pp; the 8-vectors pass between steps by readlane
+      double kr[NR];  // lane NR + a: K[a][b] = -1/2 sum_r Rq[r][a] (D^{-1} Rq)[r][b]
+      {
+        const int a = in_b ? t - NR : 0;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) acc += sm[SM::RQ + r * NR + a] * sm[SM::X + r * NR + b];
-        sm[SM::Y + q] = acc;
-      }
-      for (int d = t; d < NX; d += 64) {
-        double acc = 0.0;
+        for (int b = 0; b < NR; ++b) {
+          double acc = 0.0;
 #pragma unroll
-        for (int a = 0; a < NR; ++a) acc += P[d * NX + lr_pos(a)] * sm[SM::R8 + a];
-        cv[d] = acc;
+          for (int r = 0; r < NR; ++r) acc += sm[SM::RQ + r * NR + a] * sm[SM::X + r * NR + b];
+          kr[b] = -0.5 * acc;
+        }
       }
-      __syncthreads();
       LR_MARK(4);
-      // ---- G = -1/2 P_{:,pos} Y ------------------------------------------------
-      for (int q = t; q < NX * NR; q += 64) {
-        const int d = q / NR, b = q - d * NR;
+      auto dot8 = [](const double (&x)[NR], const double (&y)[NR]) {
         double acc = 0.0;
 #pragma unroll
-        for (int a = 0; a < NR; ++a) acc += P[d * NX + lr_pos(a)] * sm[SM::Y + a * NR + b];
-        sm[SM::G + q] = -0.5 * acc;
-      }
-      __syncthreads();
-      LR_MARK(5);
-      // ---- b = (I + 2 lam A)[(I + lam A) c + A eta0], eta += dlam (A eta + b)  (ledh.py:165-171) ----
-      apply_G(eta0, t1);  // t1 = A eta0
-      apply_G(cv, t2);    // t2 = A c
-      for (int d = t; d < NX; d += 64) t1[d] = (cv[d] + lam * t2[d]) + t1[d];  // w
-      __syncthreads();
-      apply_G(t1, t2);    // t2 = A w
-      for (int d = t; d < NX; d += 64) t1[d] = t1[d] + 2.0 * lam * t2[d];      // b
-      __syncthreads();
-      apply_G(eta, t2);   // t2 = A eta
-      for (int d = t; d < NX; d += 64) eta[d] = eta[d] + dlam * (t2[d] + t1[d]);
+        for (int b = 0; b < NR; ++b) acc += x[b] * y[b];
+        return acc;
+      };
+      double v1[NR], om_u[NR], v2[NR], dl[NR];
+      double r8a = 0.0;  // lane NR + a: r8[a]
+#pragma unroll
+      for (int a = 0; a < NR; ++a) r8a = (t == NR + a) ? r8[a] : r8a;
+      const double pr = dot8(pp, r8);
+#pragma unroll
+      for (int a = 0; a < NR; ++a) v1[a] = lam * readlane_d(pr, NR + a) + e0p[a];
+      const double ke = dot8(kr, etap);
+      const double om = r8a + dot8(kr, v1);
+#pragma unroll
+      for (int a = 0; a < NR; ++a) om_u[a] = readlane_d(om, NR + a);
+      const double po = dot8(pp, om_u);
+#pragma unroll
+      for (int a = 0; a < NR; ++a) v2[a] = readlane_d(po, NR + a);
+      const double del = (om + 2.0 * lam * dot8(kr, v2)) + ke;
+#pragma unroll
+      for (int a = 0; a < NR; ++a) dl[a] = readlane_d(del, NR + a);
+      if (t < NX) eta[t] = eta[t] + dlam * dot8(prow, dl);
       __syncthreads();
       LR_MARK(6);
     }

@@ -8,7 +8,8 @@ covariance P_0, L = n_lambda pseudo-time steps of ledh.py:136-171) the flow is i
   exact  mpmath at 40 digits, the reference's formulas (S solve, A = -1/2 P H^T S^{-1} H, b, eta);
   ref    the reference's fp64 formulas (numpy.linalg.solve on S);
   qr     the engine's k_flow_wave_lr algebra (pf_ledh_kernels.h): Householder QR of R^{-1/2} H8, the
-         8 x 8 system D X = Rq, A = -1/2 P_{:,pos} Rq^T X;
+         8 x 8 system D X = Rq, K = -1/2 Rq^T X and the update carried in the position space
+         (eta += dlam P_{:,pos} (om + 2 lam K P_pp om + K eta_pos), om = r8 + K (lam P_pp r8 + eta0_pos));
   wood   the Woodbury form through W = H8^T R^{-1} H8 (tried first, not kept).
 Prints each fp64 path's max relative error of the final eta against the exact one.  This is the
 evidence for the acoustic LEDH parity tolerances in tests/test_gpu_ledh.py.
@@ -84,10 +85,14 @@ def flow(eta0, mode):
         else:
             H8, Ppp = H[:, POS], P[np.ix_(POS, POS)]
             A = np.zeros((NX, NX))
-            if mode == "qr":
+            if mode == "qr":  # the kernel's update in the position space (A = P_{:,pos} K E)
                 Rq = householder_r(H8 / np.sqrt(RD)[:, None])
                 X = np.linalg.solve(np.eye(NR) + lam * Rq @ Ppp @ Rq.T, Rq)
-                A[:, POS] = -0.5 * P[:, POS] @ (Rq.T @ X)
+                K = -0.5 * (Rq.T @ X)
+                r8 = H8.T @ ((z - e) / RD)
+                om = r8 + K @ (lam * Ppp @ r8 + eta0[POS])
+                eta = eta + dl * (P[:, POS] @ ((om + 2 * lam * K @ (Ppp @ om)) + K @ eta[POS]))
+                continue
             else:
                 W = H8.T @ (H8 / RD[:, None])
                 A[:, POS] = -0.5 * P[:, POS] @ (W @ np.linalg.inv(np.eye(NR) + lam * Ppp @ W))

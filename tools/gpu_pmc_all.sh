@@ -25,6 +25,7 @@ for w in ${@:-sv sv64 sv_fp64 l96 mat ledh}; do
     l96) run_pmc l96 "--workload l96 --steps 50 --warmup 5" ;;
     mat) run_pmc mat "--workload mat --steps 40 --warmup 4" ;;
     ledh) run_pmc ledh "--workload ledh --steps 50 --warmup 5" ;;
+    ledh_mat) run_pmc ledh_mat "--workload ledh_mat --steps 10 --warmup 2" ;;
   esac
 done
 echo done >> "$D/steps.log"

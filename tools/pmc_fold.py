@@ -24,7 +24,8 @@ os.makedirs(OUT, exist_ok=True)
 
 # filter steps the profiled bench run covers: the warm-up W and the timed K, plus (nx > 4 with the
 # covariance) a second K-step window for the step kernels' own time, or (LEDH) a second W + K run
-STEPS = {"l96": lambda K, W: W + 2 * K, "mat": lambda K, W: W + 2 * K, "ledh": lambda K, W: 2 * (W + K)}
+STEPS = {"l96": lambda K, W: W + 2 * K, "mat": lambda K, W: W + 2 * K, "ledh": lambda K, W: 2 * (W + K),
+         "ledh_mat": lambda K, W: 2 * (W + K)}
 # name: (bench steps K, warm-up W, kernel substring, kernel_short, steps per launch for pmc_valu, SIMDs)
 LINES = {
     "sv": (20, 5, "k_resident<float, 1, 1", "k_resident", 20, None),
@@ -33,6 +34,7 @@ LINES = {
     "l96": (50, 5, "k_step_grp<float, 40, 10", "k_step_grp", 1, 1024),
     "mat": (40, 4, "k_step_grp<float, 16, 25", "k_step_grp", 1, 1024),
     "ledh": (200, 20, "k_ledh_fused", "k_ledh_fused", 1, 628),  # 157 one-wave-per-SIMD workgroups
+    "ledh_mat": (10, 2, "k_flow_wave_lr", "k_flow_wave_lr", 1, 500),  # one 64-lane workgroup per particle
 }
 for arg in sys.argv[3:]:  # name=K,W
     nm, kw = arg.split("=")
