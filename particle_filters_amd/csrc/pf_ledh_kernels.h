@@ -1215,9 +1215,8 @@ struct LrSmem {
   static constexpr int R8 = RQ + NR * NR;       // NR  H8^T R^{-1}(z - e)
   static constexpr int TT = R8 + NR;            // NR*NR  Rq P_pp
   static constexpr int X = TT + NR * NR;        // NR*NR  D^{-1} Rq
-  static constexpr int Y = X + NR * NR;         // NR*NR  Rq^T D^{-1} Rq
-  static constexpr int G = Y + NR * NR;         // NX*NR  -1/2 P_{:,pos} Rq^T D^{-1} Rq
-  static constexpr int KS = G + NX * NR;        // NR*NZ  P_pp H8^T (S of particle 0, diagnostics)
+  static constexpr int MC = X + NR * NR;        // NR*NR  M = Rq P_pp Rq^T, column-major
+  static constexpr int KS = MC + NR * NR;       // NR*NZ  P_pp H8^T (S of particle 0, diagnostics)
   static constexpr int RED = KS + NR * NZ;      // 64
   static constexpr int SIZE = RED + 64;
 };
@@ -1442,6 +1441,15 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
   const double rik = Pm[L::RI + kz * NZ + kz], zk = p.z[kz];
   // lane NR + a: row a of P_pp; lane d < NX: row d of P_{:,pos} (the flow update's operands)
   const bool in_b = t >= NR && t < 2 * NR, in_c = t >= LR_CB && t < LR_CB + NR;
+  typedef double dbl4 __attribute__((ext_vector_type(4)));
+  constexpr int KS = (NR + 3) / 4;         // k-steps of the 8 x 8 MFMA products
+  const int r16 = t & 15, kq = t >> 4;
+  double pb[KS];                           // P_pp(4 ks + kq, r16): B of Rq P_pp
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int k = 4 * ks + kq;
+    pb[ks] = (r16 < NR && k < NR) ? P[lr_pos(k) * NX + lr_pos(r16 < NR ? r16 : 0)] : 0.0;
+  }
   double pp[NR], prow[NR];
   {
     const int a = in_b ? t - NR : 0, d = t < NX ? t : 0;
@@ -1537,14 +1545,6 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
       __syncthreads();
       LR_MARK(1);
-      // TT = Rq P_pp
-      for (int q = t; q < NR * NR; q += 64) {
-        const int r = q / NR, m = q - r * NR;
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < NR; ++c) acc += sm[SM::RQ + r * NR + c] * P[lr_pos(c) * NX + lr_pos(m)];
-        sm[SM::TT + q] = acc;
-      }
       if (i == 0 && p.diagS) {  // S = lam H8 P_pp H8^T + R of particle 0 (the condition-number diagnostic)
         for (int q = t; q < NR * NZ; q += 64) {
           const int a = q / NZ, l = q - a * NZ;
@@ -1560,6 +1560,36 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
           p.diagS[(int64_t)j * NZ * NZ + q] = lam * acc + Pm[L::R + q];
         }
       }
+      // ---- M = Rq P_pp Rq^T on the fp64 matrix cores: TT = Rq P_pp, then M = TT Rq^T ------------------
+      // (v_mfma_f64_16x16x4f64 operands: A(r16, 4 ks + kq), B(4 ks + kq, r16); D(kq + 4 i, r16))
+      {
+        const bool rv = r16 < NR;
+        double ra[KS];  // Rq(r16, 4 ks + kq): A of Rq P_pp and B of TT Rq^T
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + kq;
+          ra[ks] = (rv && k < NR) ? sm[SM::RQ + r16 * NR + k] : 0.0;
+        }
+        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[ks], pb[ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (rv && kq + 4 * q < NR) sm[SM::TT + (kq + 4 * q) * NR + r16] = acc[q];
+        __syncthreads();
+        double ta[KS];  // TT(r16, 4 ks + kq)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + kq;
+          ta[ks] = (rv && k < NR) ? sm[SM::TT + r16 * NR + k] : 0.0;
+        }
+        acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ta[ks], ra[ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // column r16 of M, contiguous
+          if (rv && kq + 4 * q < NR) sm[SM::MC + r16 * NR + (kq + 4 * q)] = acc[q];
+      }
       __syncthreads();
       LR_MARK(2);
       // ---- D = I + lam Rq P_pp Rq^T, D1 = I + c1 (..), column per lane: [D | Rq] -> [I | D^{-1} Rq] ----
@@ -1569,12 +1599,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       {
         const int cc = t < NR ? t : (in_b ? t - NR : (in_c ? t - LR_CB : 0));
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          double acc = 0.0;
-#pragma unroll
-          for (int m = 0; m < NR; ++m) acc += sm[SM::TT + r * NR + m] * sm[SM::RQ + cc * NR + m];
-          m2[r] = in_b ? sm[SM::RQ + r * NR + cc] : acc;
-        }
+        for (int r = 0; r < NR; ++r) m2[r] = in_b ? sm[SM::RQ + r * NR + cc] : sm[SM::MC + cc * NR + r];
       }
       // [D | Rq | C], D = I + lam M, C = I + c1 M (det(I + dlam A) = det C / det D)
       double colD[NR];
