@@ -1225,27 +1225,49 @@ struct LrSmem {
 __device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
 
 // sums over the lanes of the sensor rows of N values at once, level by level (each DPP move reads a
-// register written N instructions earlier: no DPP hazard stalls): the lower 32 lanes when NZ <= 32
-// (one level less than a wave sum; the upper lanes hold zeros), the whole wave otherwise.  Every lane
-// ends with the sums.
+// register written several instructions earlier: no DPP hazard stalls).  NZ <= 32: the sensor rows
+// are mirrored in the upper half of the wave (lane 32 + k holds row k too), so the lower 32 lanes sum
+// the first ceil(N/2) values and the upper 32 the rest - half the DPP work, one level less than a wave
+// sum.  Otherwise the whole wave sums every value.  Every lane ends with the N sums.
 template <int NZ, int N>
 __device__ __forceinline__ void lr_row_sums(double (&v)[N]) {
+  constexpr bool SPLIT = NZ <= 32;
+  constexpr int H = SPLIT ? (N + 1) / 2 : N;
+  double w[H];
+  // the upper half's values by a bit mask (a select of two array elements becomes an indexed scratch
+  // load otherwise)
+  const long long up = (threadIdx.x & 63) >= 32 ? -1LL : 0LL;
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_QP_1032>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_QP_2301>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_HMIRROR>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_MIRROR>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_BCAST15, 0xa>(v[i]);  // rows 0, 2 not read
-  if constexpr (NZ > 32) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += dpp_mov_d<DPP_ROW_BCAST31, 0xc>(v[i]);
+  for (int j = 0; j < H; ++j) {
+    if (SPLIT && H + j < N) {
+      const long long a = __double_as_longlong(v[j]), b = __double_as_longlong(v[H + j]);
+      w[j] = __longlong_as_double((a & ~up) | (b & up));
+    } else {
+      w[j] = v[j];
+    }
   }
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = readlane_d(v[i], NZ > 32 ? 63 : 31);
+  for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_QP_1032>(w[j]);
+#pragma unroll
+  for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_QP_2301>(w[j]);
+#pragma unroll
+  for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_ROW_HMIRROR>(w[j]);
+#pragma unroll
+  for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_ROW_MIRROR>(w[j]);
+#pragma unroll
+  for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_ROW_BCAST15, 0xa>(w[j]);  // rows 0, 2 not read
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      v[j] = readlane_d(w[j], 31);
+      if (H + j < N) v[H + j] = readlane_d(w[j], 63);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < H; ++j) w[j] += dpp_mov_d<DPP_ROW_BCAST31, 0xc>(w[j]);
+#pragma unroll
+    for (int j = 0; j < H; ++j) v[j] = readlane_d(w[j], 63);
+  }
 }
 
 // Householder reflector PC of the QR of U over the wave (lane k holds row k): v = x - alpha e_PC
@@ -1435,9 +1457,11 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
   const double dlam = p.dlam;
   // lane k < NZ: sensor k's position, R_kk^{-1/2}, R_kk^{-1} (this kernel runs for a diagonal R only) and
   // z_k, loaded once instead of per pseudo-time step
-  const int kz = t < NZ ? t : 0;
+  // this lane's sensor row: NZ <= 32 mirrors the rows in the upper half of the wave (lr_row_sums)
+  const int tr = NZ <= 32 ? (t & 31) : t;
+  const int kz = tr < NZ ? tr : 0;
   const double sxk = Pm[L::AC + 2 + kz], syk = Pm[L::AC + 2 + NZ + kz];
-  const double rsk = t < NZ ? 1.0 / sqrt(Pm[L::R + kz * NZ + kz]) : 0.0;
+  const double rsk = tr < NZ ? 1.0 / sqrt(Pm[L::R + kz * NZ + kz]) : 0.0;
   const double rik = Pm[L::RI + kz * NZ + kz], zk = p.z[kz];
   // lane NR + a: row a of P_pp; lane d < NX: row d of P_{:,pos} (the flow update's operands)
   const bool in_b = t >= NR && t < 2 * NR, in_c = t >= LR_CB && t < LR_CB + NR;
@@ -1506,7 +1530,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       // lane k < NZ: row k of H8, h_k(eta), and R^{-1}(z - e) with e = h(eta) - H eta (diagonal R)
       double h8[NR];
       double ru = 0.0;
-      if (t < NZ) {
+      if (tr < NZ) {
         double acc = 0.0;
 #pragma unroll
         for (int c = 0; c < NT; ++c) {
@@ -1517,11 +1541,11 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
           h8[2 * c] = (-2.0 * psi * dx) / den2;
           h8[2 * c + 1] = (-2.0 * psi * dy) / den2;
         }
-        sm[SM::HV + t] = acc;
+        if (t < NZ) sm[SM::HV + t] = acc;
         double he = 0.0;  // H eta over the nonzero columns, in column order
 #pragma unroll
         for (int a = 0; a < NR; ++a) {
-          H8[t * NR + a] = h8[a];
+          if (t < NZ) H8[t * NR + a] = h8[a];
           he += h8[a] * etap[a];
         }
         ru = rik * (zk - (acc - he));
@@ -1539,7 +1563,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       double u[NR];
 #pragma unroll
       for (int a = 0; a < NR; ++a) u[a] = h8[a] * rsk;
-      lr_qr_col<NR, NZ, 0>(u, t);
+      lr_qr_col<NR, NZ, 0>(u, tr);
       if (t < NR)
 #pragma unroll
         for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
