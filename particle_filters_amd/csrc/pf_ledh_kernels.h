@@ -1186,15 +1186,19 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
 //   c    = P H^T R^{-1}(z - e) = P_{:,pos} H8^T R^{-1} (z - e)
 //   det(I + dlam A) = det(S - dlam/2 M) / det(S) = det(I + c1 Rq P_pp Rq^T) / det(D),  c1 = lam - dlam/2
 // (Sylvester; the reference's +1e-12 I retry is flow_logdet's c2 = lam - dlam / (2 (1 + eps)) form).
-// Per pseudo-time step the dense algebra is NR x NR (the QR, one Gauss-Jordan solve D X = Rq and one
-// LU log-determinant, in registers: lane c holds column c, the pivot column read with v_readlane)
-// instead of k_flow_wave's NZ x 2NZ Gauss-Jordan through LDS.  The QR keeps the algebra as accurate
-// as the reference's S solve: a Woodbury form through W = H8^T R^{-1} H8 squares the condition of H8
-// (W spans 1e-4 .. 4e5 next to a sensor) and lost 1e-10 per step; with the QR, a 40-digit
-// recomputation of the MAT golden's most ill-conditioned particle (cond S = 5e6) puts this algebra
-// at 3.7e-9 of the exact flow and the reference's own fp64 path at 3.1e-8
-// (tests/golden/flow_accuracy.py).  h and H evaluate as in k_flow_wave (identical expressions), so
-// do e = h - H eta and the weight terms.  Diagonal R only (the host takes k_flow_wave otherwise).
+// Per pseudo-time step the dense algebra is NR x NR: the QR (sensor rows mirrored in both half-waves,
+// each half summing half of a reflector's reductions), M = Rq P_pp Rq^T as two fp64 MFMA products,
+// and one Gauss-Jordan elimination of [D | Rq | C] in registers (column per lane, pivot columns by
+// DPP row_newbcast) that gives D^{-1} Rq and both determinants; the flow update then runs in the
+// position space (K = -1/2 Rq^T D^{-1} Rq, 8-vectors between lanes by readlane) - instead of
+// k_flow_wave's NZ x 2NZ Gauss-Jordan through LDS.  The QR keeps the algebra as accurate as the
+// reference's S solve: a Woodbury form through W = H8^T R^{-1} H8 squares the condition of H8 (W spans
+// 1e-4 .. 4e5 next to a sensor) and lost 2e-4 of the flow; with the QR, a 40-digit recomputation of
+// the MAT golden's most ill-conditioned particle (cond S = 5e6) puts this algebra at 3.3e-9 of the
+// exact flow and the reference's own fp64 path at 3.1e-8 (tools/flow_accuracy.py).  The flow's
+// reciprocals (Jacobian rows, reflector scales, pivots) are v_rcp_f64 + two Newton steps (within an
+// ulp of the division); h and the weight terms evaluate as in k_flow_wave (identical expressions).
+// Diagonal R only (the host takes k_flow_wave otherwise).
 template <int NX, int NZ>
 struct LrSmem {
   static constexpr int NR = NX / 2;             // position components: x, y of each target
@@ -1223,6 +1227,16 @@ struct LrSmem {
 
 // state index of position component a (x, y of target a / 2)
 __device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
+
+// 1 / x from v_rcp_f64 and two Newton steps (within an ulp; a third of the dependent instructions of
+// a correctly rounded division, which sits on the flow's serial chain)
+__device__ __forceinline__ double lr_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
 
 // sums over the lanes of the sensor rows of N values at once, level by level (each DPP move reads a
 // register written several instructions earlier: no DPP hazard stalls).  NZ <= 32: the sensor rows
@@ -1287,13 +1301,11 @@ __device__ __forceinline__ void lr_qr_col(double (&u)[NR], int t) {
   const double alpha = xp >= 0.0 ? -sqrt(sv[0]) : sqrt(sv[0]);
   const double vk = t == PC ? xp - alpha : xk;  // the reflector v (rows >= PC)
   const double vtv = 2.0 * alpha * (alpha - xp);
-  if (vtv > 0.0) {
-    const double beta = 2.0 / vtv;
+  const double beta = vtv > 0.0 ? 2.0 * lr_rcp(vtv) : 0.0;  // no branch: one basic block per QR
 #pragma unroll
-    for (int c = PC + 1; c < NR; ++c) {
-      const double sc = sv[c - PC] - alpha * readlane_d(u[c], PC);
-      u[c] = u[c] - beta * vk * sc;
-    }
+  for (int c = PC + 1; c < NR; ++c) {
+    const double sc = sv[c - PC] - alpha * readlane_d(u[c], PC);
+    u[c] = u[c] - beta * vk * sc;
   }
   u[PC] = t == PC ? alpha : (t > PC ? 0.0 : u[PC]);
   if constexpr (PC + 1 < NR) lr_qr_col<NR, NZ, PC + 1>(u, t);
@@ -1415,7 +1427,7 @@ __device__ __forceinline__ void lr_gj_pivot(double (&col)[NR], DetAcc& det, bool
   for (int r = 0; r < NR; ++r) f[r] = dpp_mov_d<0x150 + P>(col[r]);  // row_newbcast: lane P of this row
   det.mul(fabs(f[P]));
   ok = ok && (f[P] > 0.0);  // not positive definite after all (NaN, ...)
-  const double bp = col[P] / f[P];
+  const double bp = col[P] * lr_rcp(f[P]);
   col[P] = bp;
 #pragma unroll
   for (int r = 0; r < NR; ++r)
@@ -1536,12 +1548,11 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         for (int c = 0; c < NT; ++c) {
           const double dx = etap[2 * c] - sxk, dy = etap[2 * c + 1] - syk;
           const double den = (dx * dx + dy * dy) + d0;
-          acc += psi / den;
-          const double den2 = den * den;
-          h8[2 * c] = (-2.0 * psi * dx) / den2;
-          h8[2 * c + 1] = (-2.0 * psi * dy) / den2;
+          const double rd = lr_rcp(den), rd2 = rd * rd;
+          acc += psi * rd;
+          h8[2 * c] = (-2.0 * psi * dx) * rd2;
+          h8[2 * c + 1] = (-2.0 * psi * dy) * rd2;
         }
-        if (t < NZ) sm[SM::HV + t] = acc;
         double he = 0.0;  // H eta over the nonzero columns, in column order
 #pragma unroll
         for (int a = 0; a < NR; ++a) {
