@@ -1238,6 +1238,14 @@ __device__ __forceinline__ double lr_rcp(double x) {
   return fma(r, e, r);
 }
 
+// out[a] = x of lane NR + a, in every lane of each 16-lane row (row 0 holds the flow update's lanes):
+// DPP row_newbcast, no scalar round trip
+template <int NR, int A = 0>
+__device__ __forceinline__ void lr_row_gather(double x, double (&out)[NR]) {
+  out[A] = dpp_mov_d<0x150 + NR + A>(x);
+  if constexpr (A + 1 < NR) lr_row_gather<NR, A + 1>(x, out);
+}
+
 // sums over the lanes of the sensor rows of N values at once, level by level (each DPP move reads a
 // register written several instructions earlier: no DPP hazard stalls).  NZ <= 32: the sensor rows
 // are mirrored in the upper half of the wave (lane 32 + k holds row k too), so the lower 32 lanes sum
@@ -1707,19 +1715,17 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
       for (int a = 0; a < NR; ++a) r8a = (t == NR + a) ? r8[a] : r8a;
       const double pr = dot8(pp, r8);
+      lr_row_gather<NR>(pr, v1);
 #pragma unroll
-      for (int a = 0; a < NR; ++a) v1[a] = lam * readlane_d(pr, NR + a) + e0p[a];
+      for (int a = 0; a < NR; ++a) v1[a] = lam * v1[a] + e0p[a];
       const double ke = dot8(kr, etap);
       const double om = r8a + dot8(kr, v1);
-#pragma unroll
-      for (int a = 0; a < NR; ++a) om_u[a] = readlane_d(om, NR + a);
+      lr_row_gather<NR>(om, om_u);
       const double po = dot8(pp, om_u);
-#pragma unroll
-      for (int a = 0; a < NR; ++a) v2[a] = readlane_d(po, NR + a);
+      lr_row_gather<NR>(po, v2);
       const double del = (om + 2.0 * lam * dot8(kr, v2)) + ke;
-#pragma unroll
-      for (int a = 0; a < NR; ++a) dl[a] = readlane_d(del, NR + a);
-      if (t < NX) eta[t] = eta[t] + dlam * dot8(prow, dl);
+      lr_row_gather<NR>(del, dl);
+      if (t < NX) eta[t] = eta[t] + dlam * dot8(prow, dl);  // lanes < NX <= 16: row 0
       __syncthreads();
       LR_MARK(6);
     }
