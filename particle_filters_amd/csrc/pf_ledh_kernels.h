@@ -1221,7 +1221,9 @@ struct LrSmem {
   static constexpr int X = TT + NR * NR;        // NR*NR  D^{-1} Rq
   static constexpr int MC = X + NR * NR;        // NR*NR  M = Rq P_pp Rq^T, column-major
   static constexpr int KS = MC + NR * NR;       // NR*NZ  P_pp H8^T (S of particle 0, diagnostics)
-  static constexpr int RED = KS + NR * NZ;      // 64
+  static constexpr int UT = KS + NR * NZ;       // NZ*NR  U = R^{-1/2} H8 (the Gram's operand)
+  static constexpr int WC = UT + NZ * NR;       // NR*NR  W = U^T U, column-major
+  static constexpr int RED = WC + NR * NR;      // 64
   static constexpr int SIZE = RED + 64;
 };
 
@@ -1236,6 +1238,25 @@ __device__ __forceinline__ double lr_rcp(double x) {
   r = fma(r, e, r);
   e = fma(-x, r, 1.0);
   return fma(r, e, r);
+}
+
+// Right-looking Cholesky W = R^T R, column per lane (lane c < NR of row 0 holds column c of the trailing
+// matrix; pivot columns by DPP row_newbcast): lane c ends with column c of R in rr.  ok turns false
+// when a pivot is not above 1e-12 of its original diagonal dg (or is NaN).
+template <int NR, int P>
+__device__ __forceinline__ void lr_chol_pivot(double (&a)[NR], double (&rr)[NR], double dg, bool& ok, int c) {
+  double f[NR];
+#pragma unroll
+  for (int r = P; r < NR; ++r) f[r] = dpp_mov_d<0x150 + P>(a[r]);
+  const double d0 = dpp_mov_d<0x150 + P>(dg);
+  const double d = f[P];
+  ok = ok && (d > 1e-12 * d0);
+  const double ri = lr_rcp(sqrt(d));
+  const double rpc = c >= P ? a[P] * ri : 0.0;  // R[P][c]
+  rr[P] = rpc;
+#pragma unroll
+  for (int r = P + 1; r < NR; ++r) a[r] = a[r] - (f[r] * ri) * rpc;
+  if constexpr (P + 1 < NR) lr_chol_pivot<NR, P + 1>(a, rr, dg, ok, c);
 }
 
 // out[a] = x of lane NR + a, in every lane of each 16-lane row (row 0 holds the flow update's lanes):
@@ -1573,19 +1594,51 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         for (int a = 0; a < NR; ++a) h8[a] = 0.0;
       }
       LR_MARK(0);
-      // r8 = H8^T R^{-1}(z - e) (uniform), its wave sums issued with the QR's first column
+      if (t < NZ)
+#pragma unroll
+        for (int a = 0; a < NR; ++a) sm[SM::UT + t * NR + a] = h8[a] * rsk;
+      // r8 = H8^T R^{-1}(z - e) (uniform)
       double r8[NR];
 #pragma unroll
       for (int a = 0; a < NR; ++a) r8[a] = h8[a] * ru;
       lr_row_sums<NZ, NR>(r8);
-      // ---- Householder QR of U = R^{-1/2} H8 over the wave: lane k holds row k (NZ <= 64) -------
-      double u[NR];
+      __syncthreads();
+      // ---- Rq with Rq^T Rq = U^T U (U = R^{-1/2} H8): the Cholesky factor of the Gram W = U^T U, W on
+      // the fp64 matrix cores over the sensor rows, the factorisation column per lane (row 0).  Where W
+      // is not numerically positive definite (a pivot below 1e-12 of its diagonal), the Householder QR.
+      {
+        constexpr int KZ = (NZ + 3) / 4;
+        dbl4 g = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int a = 0; a < NR; ++a) u[a] = h8[a] * rsk;
-      lr_qr_col<NR, NZ, 0>(u, tr);
-      if (t < NR)
+        for (int ks = 0; ks < KZ; ++ks) {
+          const int k = 4 * ks + kq;
+          const double v = (r16 < NR && k < NZ) ? sm[SM::UT + k * NR + r16] : 0.0;  // U(k, r16)
+          g = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, g, 0, 0, 0);               // W += U^T U
+        }
 #pragma unroll
-        for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
+        for (int q = 0; q < 4; ++q)
+          if (r16 < NR && kq + 4 * q < NR) sm[SM::WC + r16 * NR + (kq + 4 * q)] = g[q];
+        __syncthreads();
+        double wa[NR], rr[NR];
+        const int cw = r16 < NR ? r16 : 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) wa[r] = sm[SM::WC + cw * NR + r];
+        bool okc = true;
+        lr_chol_pivot<NR, 0>(wa, rr, sm[SM::WC + cw * NR + cw], okc, r16);  // dg: W(c, c)
+        if (__builtin_amdgcn_readlane(okc ? 1 : 0, 0)) {
+          if (t < NR)
+#pragma unroll
+            for (int pr = 0; pr < NR; ++pr) sm[SM::RQ + pr * NR + t] = rr[pr];
+        } else {
+          double u[NR];
+#pragma unroll
+          for (int a = 0; a < NR; ++a) u[a] = tr < NZ ? sm[SM::UT + tr * NR + a] : 0.0;
+          lr_qr_col<NR, NZ, 0>(u, tr);
+          if (t < NR)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
+        }
+      }
       __syncthreads();
       LR_MARK(1);
       if (i == 0 && p.diagS) {  // S = lam H8 P_pp H8^T + R of particle 0 (the condition-number diagnostic)

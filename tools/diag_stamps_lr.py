@@ -34,9 +34,9 @@ assert lib.pf_debug_lr_acc(buf, 16, 1) == 0
 pf.run(st, data["Z"][1:T + 1], tracker="device")
 assert lib.pf_debug_lr_acc(buf, 16, 1) == 0
 a = np.array(buf[:10], dtype=np.float64) / 100.0  # us
-names = ["H8 rows, h, R^-1 (z - e)", "Householder QR (wave sums)", "r8, Rq P_pp (+ S of particle 0)",
-         "Gauss-Jordan [D | Rq | C], log-dets", "Y = Rq^T D^-1 Rq, c = P r8", "G = -1/2 P Y",
-         "A eta0, A c, A w, A eta, updates", "prior (g, noise) per particle", "weight + store per particle", "m2 = Rq P_pp Rq^T, [D | Rq | C]"]
+names = ["H8 rows, h, R^-1 (z - e)", "Rq: Gram (MFMA) + Cholesky", "M = Rq P_pp Rq^T (MFMA) (+ S of particle 0)",
+         "Gauss-Jordan [D | Rq | C], log-dets", "K = -1/2 Rq^T D^-1 Rq", "(unused)",
+         "position-space flow update", "prior (g, noise) per particle", "weight + store per particle", "[D | Rq | C] columns"]
 per = T * L  # pseudo-time steps of workgroup 0's first particle per filter step... (one particle per workgroup)
 tot = a.sum()
 print(f"k_flow_wave_lr workgroup 0: T={T} filter steps x L={L}, total {tot:.1f} us")

@@ -7,9 +7,12 @@ For a particle's first filter step (its x0, the reference's recorded process noi
 covariance P_0, L = n_lambda pseudo-time steps of ledh.py:136-171) the flow is integrated three ways:
   exact  mpmath at 40 digits, the reference's formulas (S solve, A = -1/2 P H^T S^{-1} H, b, eta);
   ref    the reference's fp64 formulas (numpy.linalg.solve on S);
-  qr     the engine's k_flow_wave_lr algebra (pf_ledh_kernels.h): Householder QR of R^{-1/2} H8, the
-         8 x 8 system D X = Rq, K = -1/2 Rq^T X and the update carried in the position space
+  qr     the engine's k_flow_wave_lr algebra (pf_ledh_kernels.h): Rq = the Cholesky factor of the Gram
+         W = U^T U of U = R^{-1/2} H8, the 8 x 8 system D X = Rq, K = -1/2 Rq^T X and the update carried
+         in the position space
          (eta += dlam P_{:,pos} (om + 2 lam K P_pp om + K eta_pos), om = r8 + K (lam P_pp r8 + eta0_pos));
+  hh     the same with Rq from a Householder QR of U (the kernel's fallback when W is not numerically
+         positive definite; its primary path before the Gram / Cholesky form);
   wood   the Woodbury form through W = H8^T R^{-1} H8 (tried first, not kept).
 Prints each fp64 path's max relative error of the final eta against the exact one.  This is the
 evidence for the acoustic LEDH parity tolerances in tests/test_gpu_ledh.py.
@@ -85,8 +88,9 @@ def flow(eta0, mode):
         else:
             H8, Ppp = H[:, POS], P[np.ix_(POS, POS)]
             A = np.zeros((NX, NX))
-            if mode == "qr":  # the kernel's update in the position space (A = P_{:,pos} K E)
-                Rq = householder_r(H8 / np.sqrt(RD)[:, None])
+            if mode in ("qr", "hh"):  # the kernel's update in the position space (A = P_{:,pos} K E)
+                U = H8 / np.sqrt(RD)[:, None]
+                Rq = np.linalg.cholesky(U.T @ U).T if mode == "qr" else householder_r(U)
                 X = np.linalg.solve(np.eye(NR) + lam * Rq @ Ppp @ Rq.T, Rq)
                 K = -0.5 * (Rq.T @ X)
                 r8 = H8.T @ ((z - e) / RD)
@@ -125,6 +129,6 @@ if __name__ == "__main__":
         H, _ = jac(eta0)
         cond = np.linalg.cond((1.0 / L) * H @ P @ H.T + np.diag(RD))
         ex = flow_exact(eta0)
-        errs = {m: float(np.abs(flow(eta0, m) - ex).max() / np.abs(ex).max()) for m in ("ref", "qr", "wood")}
+        errs = {m: float(np.abs(flow(eta0, m) - ex).max() / np.abs(ex).max()) for m in ("ref", "qr", "hh", "wood")}
         print(f"particle {i}: cond(S_1) {cond:.3e}; max rel error of the final eta vs 40 digits: "
               + ", ".join(f"{m} {v:.2e}" for m, v in errs.items()), flush=True)
