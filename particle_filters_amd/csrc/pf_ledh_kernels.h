@@ -1240,6 +1240,16 @@ __device__ __forceinline__ double lr_rcp(double x) {
   return fma(r, e, r);
 }
 
+// 1 / sqrt(x) from v_rsq_f64 and two Newton steps (for the Cholesky pivots: one short chain instead of
+// a correctly rounded square root and a reciprocal)
+__device__ __forceinline__ double lr_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double e = fma(-x * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, e, y);
+}
+
 // Right-looking Cholesky W = R^T R, column per lane (lane c < NR of row 0 holds column c of the trailing
 // matrix; pivot columns by DPP row_newbcast): lane c ends with column c of R in rr.  ok turns false
 // when a pivot is not above 1e-12 of its original diagonal dg (or is NaN).
@@ -1251,7 +1261,7 @@ __device__ __forceinline__ void lr_chol_pivot(double (&a)[NR], double (&rr)[NR],
   const double d0 = dpp_mov_d<0x150 + P>(dg);
   const double d = f[P];
   ok = ok && (d > 1e-12 * d0);
-  const double ri = lr_rcp(sqrt(d));
+  const double ri = lr_rsq(d);  // 1 / R[P][P]
   const double rpc = c >= P ? a[P] * ri : 0.0;  // R[P][c]
   rr[P] = rpc;
 #pragma unroll
