@@ -1230,6 +1230,11 @@ struct LrSmem {
 // state index of position component a (x, y of target a / 2)
 __device__ __forceinline__ constexpr int lr_pos(int a) { return 4 * (a >> 1) + (a & 1); }
 
+// k_flow_wave_lr's LDS hand-offs inside the lambda loop: the workgroup is one wave, and a wave's LDS
+// operations complete in issue order, so a compiler barrier orders a write before the reads that
+// follow it - no s_waitcnt drain and no s_barrier between the phases
+__device__ __forceinline__ void lr_wave_sync() { asm volatile("" ::: "memory"); }
+
 // 1 / x from v_rcp_f64 and two Newton steps (within an ulp; a third of the dependent instructions of
 // a correctly rounded division, which sits on the flow's serial chain)
 __device__ __forceinline__ double lr_rcp(double x) {
@@ -1612,7 +1617,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
       for (int a = 0; a < NR; ++a) r8[a] = h8[a] * ru;
       lr_row_sums<NZ, NR>(r8);
-      __syncthreads();
+      lr_wave_sync();
       // ---- Rq with Rq^T Rq = U^T U (U = R^{-1/2} H8): the Cholesky factor of the Gram W = U^T U, W on
       // the fp64 matrix cores over the sensor rows, the factorisation column per lane (row 0).  Where W
       // is not numerically positive definite (a pivot below 1e-12 of its diagonal), the Householder QR.
@@ -1628,7 +1633,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (r16 < NR && kq + 4 * q < NR) sm[SM::WC + r16 * NR + (kq + 4 * q)] = g[q];
-        __syncthreads();
+        lr_wave_sync();
         double wa[NR], rr[NR];
         const int cw = r16 < NR ? r16 : 0;
 #pragma unroll
@@ -1649,7 +1654,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
             for (int c = 0; c < NR; ++c) sm[SM::RQ + t * NR + c] = c >= t ? u[c] : 0.0;
         }
       }
-      __syncthreads();
+      lr_wave_sync();
       LR_MARK(1);
       if (i == 0 && p.diagS) {  // S = lam H8 P_pp H8^T + R of particle 0 (the condition-number diagnostic)
         for (int q = t; q < NR * NZ; q += 64) {
@@ -1682,7 +1687,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (rv && kq + 4 * q < NR) sm[SM::TT + (kq + 4 * q) * NR + r16] = acc[q];
-        __syncthreads();
+        lr_wave_sync();
         double ta[KS];  // TT(r16, 4 ks + kq)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -1696,7 +1701,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         for (int q = 0; q < 4; ++q)  // column r16 of M, contiguous
           if (rv && kq + 4 * q < NR) sm[SM::MC + r16 * NR + (kq + 4 * q)] = acc[q];
       }
-      __syncthreads();
+      lr_wave_sync();
       LR_MARK(2);
       // ---- D = I + lam Rq P_pp Rq^T, D1 = I + c1 (..), column per lane: [D | Rq] -> [I | D^{-1} Rq] ----
       const double c1 = lam - 0.5 * dlam;
@@ -1747,7 +1752,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       if (in_b)
 #pragma unroll
         for (int r = 0; r < NR; ++r) sm[SM::X + r * NR + (t - NR)] = colD[r];  // D^{-1} Rq
-      __syncthreads();
+      lr_wave_sync();
       LR_MARK(3);
       // ---- the flow update in the position space (ledh.py:165-171) ------------------------------
       // A v = P_{:,pos} K v_pos with K = -1/2 Rq^T D^{-1} Rq (8 x 8) and c = P_{:,pos} r8, so
@@ -1789,7 +1794,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       const double del = (om + 2.0 * lam * dot8(kr, v2)) + ke;
       lr_row_gather<NR>(del, dl);
       if (t < NX) eta[t] = eta[t] + dlam * dot8(prow, dl);  // lanes < NX <= 16: row 0
-      __syncthreads();
+      lr_wave_sync();
       LR_MARK(6);
     }
     // ---- weight (ledh.py:186-190), as k_flow_wave ---------------------------------
