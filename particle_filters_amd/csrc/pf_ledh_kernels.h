@@ -1762,14 +1762,23 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       // lane NR + a holds row a of K and of P_pp; the 8-vectors pass between steps by readlane
       double kr[NR];  // lane NR + a: K[a][b] = -1/2 sum_r Rq[r][a] (D^{-1} Rq)[r][b]
       {
+        // Rq^T (D^{-1} Rq) on the fp64 matrix cores: A(r16, k) = Rq(k, r16), B(k, r16) = X(k, r16)
+        const bool rv = r16 < NR;
+        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + kq;
+          const bool v = rv && k < NR;
+          const double av = v ? sm[SM::RQ + k * NR + r16] : 0.0, bv = v ? sm[SM::X + k * NR + r16] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // K row-major (the TT buffer is free again)
+          if (rv && kq + 4 * q < NR) sm[SM::TT + (kq + 4 * q) * NR + r16] = -0.5 * acc[q];
+        lr_wave_sync();
         const int a = in_b ? t - NR : 0;
 #pragma unroll
-        for (int b = 0; b < NR; ++b) {
-          double acc = 0.0;
-#pragma unroll
-          for (int r = 0; r < NR; ++r) acc += sm[SM::RQ + r * NR + a] * sm[SM::X + r * NR + b];
-          kr[b] = -0.5 * acc;
-        }
+        for (int b = 0; b < NR; ++b) kr[b] = sm[SM::TT + a * NR + b];
       }
       LR_MARK(4);
       auto dot8 = [](const double (&x)[NR], const double (&y)[NR]) {
