@@ -652,7 +652,7 @@ def paired_free_run(name, device=0, fixture=None):
         ora_rows.append(FR.summarise(ora, W))
     eng = {k: np.array([s[k] for s in eng_rows]) for k in eng_rows[0]}
     ora = {k: np.array([s[k] for s in ora_rows]) for k in ora_rows[0]}
-    v = FR.paired_verdict(eng, ora)
+    v = FR.paired_verdict(eng, ora, name=name)
     v.update({"config": dict(cfg), "window": f"steps [{W}, {T}) after initialize",
               "oracle": "oracle/sir_philox.py PhiloxSIROracle (fp64 NumPy restatement of particle_filter.py) on the "
                         "engine's Philox draws, tests/golden/free_run_pairs.npz (make_golden_free_run.py)"})
@@ -975,8 +975,9 @@ def main():
                         pv, _, _ = paired_free_run(wl.name, device=local)
                         ref["paired_free_run"] = pv
                         ref["tolerance"] = ("paired free runs: mean per-replicate difference (engine - fp64 oracle, "
-                                            "same Philox draws) of every statistic within 3 standard errors "
-                                            "(SURVEY 8(c)(i))")
+                                            "same Philox draws) of every statistic within 3 standard errors and "
+                                            "within the stated relative margin (oracle/free_run.MARGINS), with "
+                                            "3 SE / |oracle mean| <= that margin (SURVEY 8(c)(i))")
                         ref["parity_ok"] = pv["ok"]
                     except Exception as e:
                         ref["paired_free_run"] = {"error": repr(e)}

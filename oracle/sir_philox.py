@@ -43,10 +43,14 @@ OBS_LINEAR, OBS_EXP_HALF, OBS_SV_EXACT = 0, 1, 3
 class PhiloxRNG:
     """Serves the engine's device draws for the (epoch, stream) set by the caller."""
 
-    def __init__(self, seed: int, rep: int = 0, bm24: bool = True):
+    def __init__(self, seed: int, rep: int = 0, bm24: bool = True, c_normals: bool = False):
         self.seed = int(seed)
         self.rep = int(rep)
         self.bm24 = bool(bm24)
+        # c_normals: the same draws from the C restatement (pfo_normals, ~20x faster; its libm
+        # sin / cos differ from NumPy's in the last ulp on ~0.2 % of the values) - used by the
+        # statistical free-run pairs (oracle/free_run.py), where one ulp is immaterial
+        self.c_normals = bool(c_normals)
         self.epoch: Optional[int] = None
         self.stream: Optional[int] = None
 
@@ -57,8 +61,11 @@ class PhiloxRNG:
     def standard_normal(self, size=None):
         shape = () if size is None else tuple(np.atleast_1d(size))
         n = int(np.prod(shape)) if shape else 1
-        v = philox.normals(self.seed, n, self.rep, self.epoch, self.stream,
-                           dtype=np.float32 if self.bm24 else np.float64)
+        if self.c_normals:
+            v = normals(self.seed, n, self.rep, self.epoch, self.stream, bm24=self.bm24)
+        else:
+            v = philox.normals(self.seed, n, self.rep, self.epoch, self.stream,
+                               dtype=np.float32 if self.bm24 else np.float64)
         return v.reshape(shape) if shape else float(v[0])
 
     def random(self, size=None):
@@ -74,8 +81,9 @@ class PhiloxSIROracle(SIROracle):
     """``SIROracle`` on the engine's Philox draws (epochs of pf_engine.hip: one per
     initialize / predict / update)."""
 
-    def __init__(self, g, h, Q, R, *, seed: int, rep: int = 0, bm24: bool = True, epoch: int = 1, **kw):
-        self.prng = PhiloxRNG(seed, rep, bm24)
+    def __init__(self, g, h, Q, R, *, seed: int, rep: int = 0, bm24: bool = True, epoch: int = 1,
+                 c_normals: bool = False, **kw):
+        self.prng = PhiloxRNG(seed, rep, bm24, c_normals)
         super().__init__(g, h, Q, R, rng=self.prng, **kw)
         self.epoch = int(epoch)
         self.forced = None  # optional per-step decisions (teacher forcing), consumed in order

@@ -83,8 +83,11 @@ def sv_logsq(alpha: float, sigma: float, beta: float) -> SSM:
 
 
 def l96_rhs(x, F):
-    """simulator_Lorenz_96.py:35-59 along the last axis."""
-    return (np.roll(x, -1, axis=-1) - np.roll(x, 2, axis=-1)) * np.roll(x, 1, axis=-1) - x + F
+    """simulator_Lorenz_96.py:35-59 along the last axis: (x[i+1] - x[i-2]) x[i-1] - x[i] + F, cyclic
+    (one wrapped copy instead of three np.roll copies; bitwise the same values)."""
+    n = x.shape[-1]
+    xp = np.concatenate([x[..., -2:], x, x[..., :1]], axis=-1)  # xp[j] = x[j - 2]
+    return (xp[..., 3:n + 3] - xp[..., 0:n]) * xp[..., 1:n + 1] - x + F
 
 
 def l96_rk4(x, dt, F):

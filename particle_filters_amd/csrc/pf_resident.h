@@ -87,8 +87,8 @@ constexpr unsigned RSPIN_LIMIT = 1u << 24;
 #endif
 constexpr int RSTAGE = PF_RSTAGE;  // rollback scatter staging chunk (floats of LDS)
 
-// Diagnostic phase accounting (PF_STAMPS builds only): workgroup 0, thread 0
-// accumulates s_memrealtime ticks (100 MHz) per phase into g_pf_stamps[0..15].
+// Diagnostic phase accounting (PF_STAMPS builds only): one thread (PF_STAMP_T of workgroup
+// PF_STAMP_B) accumulates s_memrealtime ticks (100 MHz) per phase into g_pf_stamps[0..15, 22, 23].
 #ifdef PF_STAMPS
 // accumulated in registers (thread 0 of workgroup 0), written once at the end
 #define PF_RMARK(k)                                                     \
@@ -557,8 +557,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   __shared__ __attribute__((aligned(16))) float mmax[2][RNW];  // the wave maxima again, for one vector read
   __shared__ double cslot[2][RCW][8];  // the verified step's summary (+ tags-complete flag)
   __shared__ int okw[RNW];
+  __shared__ double auxw[RNW][2];  // wave sums of the freshly resampled state (x, x^2): the next record's aux
   __shared__ double sF[NSNAP];     // frame of each snapshot slot
-  __shared__ long long sT[NSNAP];  // filter step of each snapshot slot
+  __shared__ int sT[NSNAP];  // filter step of each snapshot slot
   __shared__ double Pl[RMAXG + 1];
   __shared__ double Ck[RMAXG];
   __shared__ double offs[RBS];
@@ -586,10 +587,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   const size_t cstride = gran_copy_stride(R);
   // this workgroup's replica of its replicate's record ring (reads), and replica 0
   const unsigned long long* gbase = p.gran + (size_t)(b % RCOPIES) * cstride + (size_t)r * RRING * RF * RMAXG;
-  const unsigned long long* gbase0 = p.gran + (size_t)r * RRING * RF * RMAXG;
   if (t == 0) err_sh = 0;
-  const unsigned long long total_wg = (unsigned long long)gridDim.x * gridDim.y;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  __shared__ unsigned long long t_start_sh;  // for the slow polls' 1 ms check (not held in registers)
+  if (t == 0) t_start_sh = t_start;
   __shared__ int arr_sh;
   if (p.test_abort && b == p.G - 1 && blockIdx.y == 0) {  // test hook: arrive after the others gave up
     if (t == 0)
@@ -603,10 +604,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 #ifndef PF_STAMP_T
 #define PF_STAMP_T 0
 #endif
-  const bool stamp_me = b == 0 && r == 0 && t == PF_STAMP_T;  // PF_STAMP_T: the stamped thread (wave)
-  unsigned long long racc[16];
+#ifndef PF_STAMP_B
+#define PF_STAMP_B 0
+#endif
+  // PF_STAMP_T: the stamped thread (wave); PF_STAMP_B: the stamped workgroup (-1: the output one)
+  const bool stamp_me = (PF_STAMP_B < 0 ? b == p.G - 1 : b == PF_STAMP_B) && r == 0 && t == PF_STAMP_T;
+  unsigned long long racc[24];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) racc[k] = 0;
+  for (int k = 0; k < 24; ++k) racc[k] = 0;
   unsigned long long rstamp_last = __builtin_amdgcn_s_memrealtime();
 #endif
 
@@ -614,6 +619,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   // loads and reduces the moment / aux granules) and for all others.  A compile-time flag
   // keeps the granule loads unconditional inside one uniform branch, so their registers need
   // no merge copies (a copy right after the loads would wait for them at the loop top).
+  // Kernel arguments that only cold paths use (rollback, outputs, slow polls, trace, exit) are
+  // re-read from the kernarg segment where they are used, through a pointer the compiler cannot
+  // hoist: carried around the loop they cost ~100 scalar registers, spilled and reloaded in the
+  // step loop.
+  auto KA = []() {
+    typedef const __attribute__((address_space(4))) ResParams CRes;
+    CRes* q = (CRes*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return q;
+  };
   auto body = [&, p](auto out_tag) {  // p by value: its fields stay in registers, not kernarg reloads
   constexpr bool outwg = decltype(out_tag)::value;  // b == G - 1
   // ---- entry state (k_step layout) and its normaliser ------------------------
@@ -653,7 +668,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
     }
     if (!have_hdr) {
-      const Head h0 = prologue<NX, RBS>(p.rec_in + (int64_t)r * RC::SIZE * p.Gk, p.Gk, N, p.thresh, false, false,
+      const Head h0 = prologue<NX, RBS>(p.rec_in + (int64_t)r * RC::SIZE * KA()->Gk, KA()->Gk, N, p.thresh, false, false,
                                         false, red, Pl);
       lse0d = uni(h0.lse);
       uniform0 = h0.uniform != 0;
@@ -667,7 +682,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       l[e] = (i0 + e >= N) ? -INFINITY : (uniform0 ? lunif : (have_hdr ? lr[e] : lr[e] - lse0));
     if (uniform0) F0 = T0 = 0.0;
   }
-  if (t == 0) arr_sh = arr_old - p.arrive0 < RABORT;  // arrived after an abort: leave
+  if (t == 0) arr_sh = arr_old - KA()->arrive0 < RABORT;  // arrived after an abort: leave
   __syncthreads();
   if (!arr_sh) return;
 #ifdef PF_STAMPS
@@ -679,7 +694,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool verified_any = false;  // a verified step proves the whole grid has arrived
 
   const int fo = p.first_update_only ? 1 : 0;
-  int64_t tstep = 0;       // next filter step to compute
+  const int T32 = (int)p.T;  // the host keeps T < 2^30
+  int tstep = 0;           // next filter step to compute
   unsigned s_next = 0;     // next sequence number (executed steps, incl. discarded ones)
   unsigned vnext = 0;      // next sequence number to verify
   unsigned nres = 0;       // hand-offs so far (flag tags)
@@ -693,28 +709,26 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   bool prev_res = false;   // last verified step resampled: next record carries its aux sums
   bool have_aux = false;   // the live state was just gathered
   bool rec_aux = false;    // the record being published carries the aux sums
-  double aux1 = 0.0, aux2 = 0.0;
   bool last_uniform = false;
   bool alive = true;
   bool aborted = false;
   double Tlast = T0;    // absolute log mass of the last verified (not resampled) step
-  int last_cur = 0;     // mslot buffer of the last computed step, and its frame
-  double F_last = F0;
+  int last_cur = 0;     // mslot buffer of the last computed step (its frame: sF of its snapshot slot)
   float zwin = 0.0f;    // observation window (NZ == 1): lane k holds z of step zbase + k
-  int64_t zbase = -64;
+  int zbase = -64;
   while (alive) {
     // granules of the step this iteration verifies (waves 0..RCW-1: one record per lane); per
     // iteration, so they are not carried around the loop (and through the rollback) in VGPRs.
     // Left undefined where not loaded: a zero default would merge with the loaded values.
     unsigned long long pg[RF];
-    const bool computing = tstep < p.T;
+    const bool computing = tstep < T32;
     const unsigned s_after = s_next + (computing ? 1u : 0u);
 #if defined(PF_ABLATE) && PF_ABLATE == 1
     const bool verify = false;  // ablation: no verification at all (timing floor of the step)
     if (!computing) break;
 #else
     const bool verify =
-        vnext < s_after && (s_after - vnext > (unsigned)LAG || tstep + (computing ? 1 : 0) >= p.T);
+        vnext < s_after && (s_after - vnext > (unsigned)LAG || tstep + (computing ? 1 : 0) >= T32);
 #endif
     if (!computing && !verify) break;
     // observations: a window of 64 steps in one VGPR (lane k: step zbase + k), read per step
@@ -722,8 +736,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     // across its start) - no memory wait in the step
     if (NZ == 1 && computing && (tstep < zbase || tstep >= zbase + 64)) {
       zbase = tstep;
-      const int64_t tl = tstep + lane;
-      zwin = tl < p.T ? p.z[(size_t)tl * R + r] : 0.0f;
+      const int tl = tstep + lane;
+      zwin = tl < T32 ? KA()->z[(size_t)tl * R + r] : 0.0f;
       // wait for it here, in the rare branch: otherwise the wait lands before every step's
       // readlane and (vmcnt counts in order) takes the granule loads issued below with it
       asm volatile("; z window %0" ::"v"(zwin));
@@ -735,7 +749,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     const unsigned long long* vbase = gbase + (size_t)(v % RRING) * RF * RMAXG + t;
     const int idx = (int)(v % NSNAP);  // snapshot slot of step v
     double Fv = 0.0;
-    int64_t tv = 0;
+    int tv = 0;
     if (verify) {
       // granule loads for v (their latency overlaps the step below); slot info
       // read before this iteration's barrier (written iterations ago)
@@ -750,7 +764,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         tv = tstep;
       } else {
         Fv = uni(sF[idx]);
-        tv = uni_i64(sT[idx]);
+        tv = __builtin_amdgcn_readfirstlane(sT[idx]);
       }
     }
     // the step's observation (and control) are uniform: scalar loads through the constant
@@ -835,9 +849,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       const float w1 = wave_sum_u(s1 * fw), w2 = wave_sum_u(s2 * fw);
       double a1 = 0.0, a2 = 0.0;
       if (have_aux) {
-        a1 = wave_sum_ud(aux1);
-        a2 = wave_sum_ud(aux2);
+        a1 = auxw[w][0];
+        a2 = auxw[w][1];
       }
+      PF_RMARK(22);  // the wave's own partials (DPP)
       if (lane == 0) {
         mmax[cur][w] = Mw;
         mslot[cur][w][0] = Mw;
@@ -862,8 +877,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       }
       rec_aux = have_aux;
       have_aux = false;
-      last_cur = cur;  // exit records: this step's wave partials and frame
-      F_last = F;
+      last_cur = cur;  // exit records: this step's wave partials
     }
 
     // ---------------- wave-level summary of the step being verified ----------
@@ -906,6 +920,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         cslot[cur][w][7] = wgood ? 1.0 : 0.0;
       }
     }
+    PF_RMARK(23);  // the verification summary (waits for the granule loads)
     __syncthreads();  // the iteration's one barrier
 #ifdef PF_YOUNG_PRIO
     if (w >= RCW && w != PF_PUBW) __builtin_amdgcn_s_setprio(0);
@@ -987,9 +1002,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     for (unsigned spins = 0; !all; ++spins) {  // slow path: not every record was in yet
       PF_RCOUNT(15);
       __syncthreads();  // every wave has read cslot[cur]
-      if (!verified_any && (spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t_start > RARRIVE_TICKS) {
+      if (!verified_any && (spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS) {
         // still no step verified after 1 ms: is the grid resident at all?
-        if (t == 0) arr_sh = res_try_abort(p.arrive, p.err, p.arrive0, total_wg, p.seq) ? 2 : 1;
+        if (t == 0) arr_sh = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)gridDim.x * gridDim.y, KA()->seq) ? 2 : 1;
         __syncthreads();
         if (arr_sh == 2) {
           aborted = true;
@@ -1001,7 +1016,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       if (spins >= RSPIN_LIMIT) {
         if (t == 0) {
           err_sh = 1;
-          atomicOr(p.err, 1u);
+          atomicOr(KA()->err, 1u);
         }
         alive = false;
         break;
@@ -1056,11 +1071,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       if (t == 0) {
         int res = 0;
         while (res == 0) {
-          const unsigned long long rel = ld_sc1(p.arrive) - p.arrive0;
+          const unsigned long long rel = ld_sc1(KA()->arrive) - KA()->arrive0;
           if (rel >= RABORT) res = 2;
-          else if (rel >= total_wg) res = 1;
-          else if (__builtin_amdgcn_s_memrealtime() - t_start > RARRIVE_TICKS)
-            res = res_try_abort(p.arrive, p.err, p.arrive0, total_wg, p.seq) ? 2 : 1;
+          else if (rel >= (unsigned long long)gridDim.x * gridDim.y) res = 1;
+          else if (__builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS)
+            res = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)gridDim.x * gridDim.y, KA()->seq) ? 2 : 1;
           else
             __builtin_amdgcn_s_sleep(2);
         }
@@ -1098,14 +1113,14 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       // every particle's weight is zero or NaN (e.g. an all -inf log-likelihood,
       // SURVEY 8c(vi)): the filter is dead.  Every workgroup reduces the same records
       // to the same W, so all of them stop here; the host reports PF_E_NAN.
-      if (b == G - 1 && t == 0) {
-        const int64_t o = tv * R + r;
-        p.o_neff[o] = __builtin_nan("");
-        p.o_lse[o] = __builtin_nan("");
-        p.o_mean[o] = __builtin_nan("");
-        if (p.o_cov) p.o_cov[o] = __builtin_nan("");
-        p.o_flag[o] = 0;
-        atomicOr(p.err, 8u);
+      if (outwg && t == 0) {
+        const int64_t o = (int64_t)tv * R + r;
+        KA()->o_neff[o] = __builtin_nan("");
+        KA()->o_lse[o] = __builtin_nan("");
+        KA()->o_mean[o] = __builtin_nan("");
+        if (KA()->o_cov) KA()->o_cov[o] = __builtin_nan("");
+        KA()->o_flag[o] = 0;
+        atomicOr(KA()->err, 8u);
       }
       alive = false;
       break;
@@ -1118,34 +1133,34 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 #endif
     const double Tv = lse_rel + Fv;
     if constexpr (TR) {  // trace build: the verified step's predicted state, from its snapshot
-      if (tv < p.tr_T) {
-        const size_t to = ((size_t)tv * R + r) * (size_t)p.Npad;
+      if (tv < KA()->tr_T) {
+        const size_t to = ((size_t)tv * R + r) * (size_t)KA()->Npad;
 #pragma unroll
         for (int q = 0; q < RPV; ++q) {
           const float4 xs = snx[idx][q * RBS + t], ls = snl[idx][q * RBS + t];
           const float xa[4] = {xs.x, xs.y, xs.z, xs.w}, la[4] = {ls.x, ls.y, ls.z, ls.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (i0 + 4 * q + e < p.Npad) {
-              p.tr_x[to + i0 + 4 * q + e] = xa[e];
-              p.tr_l[to + i0 + 4 * q + e] = la[e];
+            if (i0 + 4 * q + e < KA()->Npad) {
+              KA()->tr_x[to + i0 + 4 * q + e] = xa[e];
+              KA()->tr_l[to + i0 + 4 * q + e] = la[e];
             }
         }
       }
     }
-    if (b == G - 1 && t == 0) {  // outputs: the last workgroup (the partial tile, least work)
-      const int64_t o = tv * R + r;
-      p.o_neff[o] = (W * W) / W2;
-      p.o_lse[o] = Tv - Tprev;
-      p.o_flag[o] = dec ? 1 : 0;
+    if (outwg && t == 0) {  // outputs: the last workgroup (the partial tile, least work)
+      const int64_t o = (int64_t)tv * R + r;
+      KA()->o_neff[o] = (W * W) / W2;
+      KA()->o_lse[o] = Tv - Tprev;
+      KA()->o_flag[o] = dec ? 1 : 0;
       const double mean = S1 / W;
-      p.o_mean[o] = mean;
-      if (p.o_cov) p.o_cov[o] = S2 / W - mean * mean;
+      KA()->o_mean[o] = mean;
+      if (KA()->o_cov) KA()->o_cov[o] = S2 / W - mean * mean;
       if (prev_res) {  // post-resample moments of step tv - 1 (uniform weights)
-        const int64_t o2 = (tv - 1) * R + r;
+        const int64_t o2 = (int64_t)(tv - 1) * R + r;
         const double mp = A1 / (double)N;
-        p.o_mean[o2] = mp;
-        if (p.o_cov) p.o_cov[o2] = A2 / (double)N - mp * mp;
+        KA()->o_mean[o2] = mp;
+        if (KA()->o_cov) KA()->o_cov[o2] = A2 / (double)N - mp * mp;
       }
     }
     prev_res = false;
@@ -1164,10 +1179,10 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     PF_RCOUNT(13);
     ++nres;
     const uint32_t ep_res = p.ep0 + (uint32_t)(2 * tv + 1) - fo;
-    if (!rb_gather<Real, NX, NZ, TK, OK>(p.xg + rN, p.sflag + (size_t)r * RMAXG, p.flag0,
-                                          p.err, &err_sh, snx[idx], snl[idx], red, Pl, Ck, offs, stage, G, b, N, nres, m_g,
-                                          s0_g, Mx, p.seed, rep, ep_res, p.regularize, (const Real*)p.P,
-                                          (TR && tv < p.tr_T) ? p.tr_anc + ((size_t)tv * R + r) * (size_t)p.Npad
+    if (!rb_gather<Real, NX, NZ, TK, OK>(KA()->xg + rN, KA()->sflag + (size_t)r * RMAXG, KA()->flag0,
+                                          KA()->err, &err_sh, snx[idx], snl[idx], red, Pl, Ck, offs, stage, G, b, N, nres, m_g,
+                                          s0_g, Mx, p.seed, rep, ep_res, KA()->regularize, (const Real*)KA()->P,
+                                          (TR && tv < KA()->tr_T) ? KA()->tr_anc + ((size_t)tv * R + r) * (size_t)KA()->Npad
                                                               : (int32_t*)nullptr)) {
       alive = false;
       break;
@@ -1180,17 +1195,25 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       x[4 * q + 2] = xs.z;
       x[4 * q + 3] = xs.w;
     }
-    aux1 = 0.0;
-    aux2 = 0.0;
+    {
+      double aux1 = 0.0, aux2 = 0.0;
 #pragma unroll
-    for (int e = 0; e < RPPT; ++e) {
-      if (i0 + e < N) {
-        l[e] = lunif;
-        aux1 += (double)x[e];
-        aux2 += (double)x[e] * (double)x[e];
-      } else {
-        x[e] = 0.0f;
-        l[e] = -INFINITY;
+      for (int e = 0; e < RPPT; ++e) {
+        if (i0 + e < N) {
+          l[e] = lunif;
+          aux1 += (double)x[e];
+          aux2 += (double)x[e] * (double)x[e];
+        } else {
+          x[e] = 0.0f;
+          l[e] = -INFINITY;
+        }
+      }
+      // their wave sums now, kept in LDS until the next record (not in registers around the loop)
+      aux1 = wave_sum_ud(aux1);
+      aux2 = wave_sum_ud(aux2);
+      if (lane == 0) {
+        auxw[w][0] = aux1;
+        auxw[w][1] = aux2;
       }
     }
     PF_RMARK(5);
@@ -1209,27 +1232,21 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
 #endif
   // ---- the last step resampled: its post-resample moments -------------------
   if (alive && prev_res) {
-    const double a1 = wave_sum_ud(aux1), a2 = wave_sum_ud(aux2);
-    __syncthreads();
-    if (lane == 0) {
-      mslot[0][w][5] = a1;
-      mslot[0][w][6] = a2;
-    }
     __syncthreads();
     if (t == 0) {
       double A1 = 0.0, A2 = 0.0;
       for (int j = 0; j < RNW; ++j) {
-        A1 += mslot[0][j][5];
-        A2 += mslot[0][j][6];
+        A1 += auxw[j][0];
+        A2 += auxw[j][1];
       }
       const unsigned tag = p.tag0 + s_next + 1;
-      unsigned long long* g = p.gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
+      unsigned long long* g = KA()->gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + b;
       st_sc1(g + 5 * RMAXG, granule(tag, (float)A1));
       st_sc1(g + 6 * RMAXG, granule(tag, (float)A2));
     }
     // every workgroup's aux granules (fixed-order sum in each workgroup)
     const unsigned tag = p.tag0 + s_next + 1;
-    const unsigned long long* base = gbase0 + (size_t)(s_next % RRING) * RF * RMAXG + t;  // replica 0
+    const unsigned long long* base = KA()->gran + ((size_t)r * RRING + s_next % RRING) * RF * RMAXG + t;  // replica 0
     for (unsigned spins = 0;; ++spins) {
       int good = 1;
       unsigned long long g5 = 0, g6 = 0;
@@ -1255,22 +1272,22 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           }
         }
         __syncthreads();
-        if (b == G - 1 && t == 0) {
+        if (outwg && t == 0) {
           double S5 = 0.0, S6 = 0.0;
           for (int j = 0; j < RCW; ++j) {
             S5 += cslot[0][j][5];
             S6 += cslot[0][j][6];
           }
-          const int64_t o2 = (p.T - 1) * R + r;
+          const int64_t o2 = (KA()->T - 1) * R + r;
           const double mp = S5 / (double)N;
-          p.o_mean[o2] = mp;
-          if (p.o_cov) p.o_cov[o2] = S6 / (double)N - mp * mp;
+          KA()->o_mean[o2] = mp;
+          if (KA()->o_cov) KA()->o_cov[o2] = S6 / (double)N - mp * mp;
         }
         break;
       }
       __syncthreads();
       if (spins >= RSPIN_LIMIT) {
-        if (t == 0) atomicOr(p.err, 4u);
+        if (t == 0) atomicOr(KA()->err, 4u);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -1281,15 +1298,15 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   if (i0 + RPPT <= N) {
 #pragma unroll
     for (int q4 = 0; q4 < RPV; ++q4) {
-      *(float4*)(p.x_fin + rN + i0 + 4 * q4) = make_float4(x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]);
-      *(float4*)(p.lw_fin + rN + i0 + 4 * q4) = make_float4(l[4 * q4], l[4 * q4 + 1], l[4 * q4 + 2], l[4 * q4 + 3]);
+      *(float4*)(KA()->x_fin + rN + i0 + 4 * q4) = make_float4(x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]);
+      *(float4*)(KA()->lw_fin + rN + i0 + 4 * q4) = make_float4(l[4 * q4], l[4 * q4 + 1], l[4 * q4 + 2], l[4 * q4 + 3]);
     }
   } else {
 #pragma unroll
     for (int e = 0; e < RPPT; ++e)
       if (i0 + e < N) {
-        p.x_fin[rN + i0 + e] = x[e];
-        p.lw_fin[rN + i0 + e] = l[e];
+        KA()->x_fin[rN + i0 + e] = x[e];
+        KA()->lw_fin[rN + i0 + e] = l[e];
       }
   }
 #ifdef PF_STAMPS
@@ -1303,11 +1320,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
     static_assert(KW >= 1 && KQ % 64 == 0, "k_step tiles of whole waves");
     const int q = t / KQ;
     const int kt = b * (RTILE / 1024) + q;
-    if ((t % KQ) == 0 && kt < p.Gk) {
-      double* o = p.rec_fin + (int64_t)r * RC::SIZE * p.Gk;
-      for (int f2 = 0; f2 < RC::SIZE; ++f2) o[(int64_t)f2 * p.Gk + kt] = 0.0;
+    if ((t % KQ) == 0 && kt < KA()->Gk) {
+      double* o = KA()->rec_fin + (int64_t)r * RC::SIZE * KA()->Gk;
+      for (int f2 = 0; f2 < RC::SIZE; ++f2) o[(int64_t)f2 * KA()->Gk + kt] = 0.0;
       if (last_uniform) {
-        o[(int64_t)RC::UNI * p.Gk + kt] = 1.0;
+        o[(int64_t)RC::UNI * KA()->Gk + kt] = 1.0;
       } else {
         const double(*ms)[8] = mslot[last_cur];
         double Mq = -INFINITY;
@@ -1321,11 +1338,12 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
           s1 += ms[KW * q + j][3] * fj;
           s2 += ms[KW * q + j][4] * fj;
         }
-        o[(int64_t)RC::M * p.Gk + kt] = Mq - (F - F_last);
-        o[(int64_t)RC::S0 * p.Gk + kt] = s0;
-        o[(int64_t)RC::S00 * p.Gk + kt] = s00;
-        o[(int64_t)RC::S1 * p.Gk + kt] = s1;
-        if constexpr (RC::COV) o[(int64_t)RC::S2 * p.Gk + kt] = s2;
+        const double F_last = sF[(s_next - 1) % NSNAP];  // the last computed step's frame
+        o[(int64_t)RC::M * KA()->Gk + kt] = Mq - (F - F_last);
+        o[(int64_t)RC::S0 * KA()->Gk + kt] = s0;
+        o[(int64_t)RC::S00 * KA()->Gk + kt] = s00;
+        o[(int64_t)RC::S1 * KA()->Gk + kt] = s1;
+        if constexpr (RC::COV) o[(int64_t)RC::S2 * KA()->Gk + kt] = s2;
       }
     }
   }
@@ -1333,16 +1351,16 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   // mass Tlast (the exit log-weights sum to e^(Tlast - F): the fp32 residual of the final shift),
   // or uniform
   if (b == 0 && t == 0 && alive) {
-    unsigned long long* hp = p.hdr + (size_t)r * 4;
+    unsigned long long* hp = KA()->hdr + (size_t)r * 4;
     hp[1] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : Tlast);
     hp[2] = last_uniform ? 1ull : 0ull;
     hp[3] = (unsigned long long)__double_as_longlong(last_uniform ? 0.0 : F);
-    hp[0] = p.hdr_out;
+    hp[0] = KA()->hdr_out;
   }
 #ifdef PF_STAMPS
   if (stamp_me)
-    for (int k = 0; k < 16; ++k)
-      if (k < 6 || k > 11) g_pf_stamps[k] = racc[k];
+    for (int k = 0; k < 24; ++k)
+      if (k < 6 || (k > 11 && k < 16) || k > 21) g_pf_stamps[k] = racc[k];
   if (b == 0 && r == 0 && t == 0) g_pf_stamps[19] = __builtin_amdgcn_s_memrealtime();
 #endif
   };

@@ -13,14 +13,42 @@ from tests.conftest import load_golden
 def test_paired_verdict_arithmetic():
     rng = np.random.default_rng(0)
     o = rng.normal(1.0, 0.1, 32)
-    same = FR.paired_verdict({"rmse": o.copy()}, {"rmse": o})
+    m = {"rmse": 0.05}
+    same = FR.paired_verdict({"rmse": o.copy()}, {"rmse": o}, margins=m)
     assert same["ok"] and same["rmse"]["mean_paired_diff"] == 0.0
-    noisy = FR.paired_verdict({"rmse": o + rng.normal(0, 0.01, 32)}, {"rmse": o})
-    assert noisy["ok"] and abs(noisy["rmse"]["z"]) < 3
-    biased = FR.paired_verdict({"rmse": o + 0.05 + rng.normal(0, 0.01, 32)}, {"rmse": o})
+    noisy = FR.paired_verdict({"rmse": o + rng.normal(0, 0.01, 32)}, {"rmse": o}, margins=m)
+    assert noisy["ok"] and abs(noisy["rmse"]["z"]) < 3 and noisy["rmse"]["powered"]
+    biased = FR.paired_verdict({"rmse": o + 0.05 + rng.normal(0, 0.01, 32)}, {"rmse": o}, margins=m)
     assert not biased["ok"] and biased["rmse"]["z"] > 3
     with pytest.raises(ValueError):
-        FR.paired_verdict({"rmse": o[:3]}, {"rmse": o})
+        FR.paired_verdict({"rmse": o[:3]}, {"rmse": o}, margins=m)
+    with pytest.raises(ValueError):
+        FR.paired_verdict({"rmse": o}, {"rmse": o})  # no margins and no configuration name
+
+
+def test_paired_verdict_margin_and_power():
+    """The stated margin binds even when the bias hides in the noise, and a check too noisy to see a
+    bias of the margin's size fails as unpowered (oracle/free_run.py paired_verdict)."""
+    rng = np.random.default_rng(1)
+    o = rng.normal(1.0, 0.1, 64)
+    m = {"rmse": 0.05}
+    # a 6 % bias with large paired noise: within 3 SE, but over the margin and unpowered
+    hidden = FR.paired_verdict({"rmse": o * 1.06 + rng.normal(0, 0.5, 64)}, {"rmse": o}, margins=m)["rmse"]
+    assert not hidden["powered"] and not hidden["ok"]
+    # a 6 % bias with little noise: powered, outside both the SE band and the margin
+    clear = FR.paired_verdict({"rmse": o * 1.06 + rng.normal(0, 0.005, 64)}, {"rmse": o}, margins=m)["rmse"]
+    assert clear["powered"] and not clear["within_margin"] and not clear["ok"]
+    # a 1 % bias with little noise: powered and within the margin, but resolved by the SE band
+    small = FR.paired_verdict({"rmse": o * 1.01 + rng.normal(0, 0.001, 64)}, {"rmse": o}, margins=m)["rmse"]
+    assert small["powered"] and small["within_margin"] and not small["within_se"]
+    assert abs(small["detectable_bias_rel"] - 3 * small["se_paired_diff"] / abs(small["oracle_mean"])) < 1e-15
+
+
+def test_margins_cover_every_statistic():
+    for name in FR.CONFIGS:
+        need = {"rmse", "loglik", "resample_rate"} | ({"omat"} if FR.CONFIGS[name].get("n_targets") else set())
+        assert need <= set(FR.MARGINS[name]), name
+        assert all(0 < v <= 0.25 for v in FR.MARGINS[name].values())
 
 
 def test_summarise_window_and_omat():
