@@ -210,6 +210,16 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
  * grid co-resident), 0 if as the launch-per-step loop.  PF_RESIDENT=0 in the
  * environment forces the launch-per-step loop. */
 int32_t pf_last_run_resident(pf_handle* h);
+/* Uninitialised-LDS test hooks (tests/test_gpu_lds_poison.py; no reference counterpart):
+ * pf_test_lds_poison fills the whole 160 KB of LDS of every CU with 0xFFFFFFFF (NaN in fp32 and
+ * fp64) on `stream` (a hipStream_t); with PF_TEST_HOOKS=1 and PF_TEST_LDS_POISON=1 in the
+ * environment the engine does the same before every launch of its LDS-staging step, flow, EKF and
+ * covariance kernels.  pf_test_lds_probe launches pf_test_lds_probe_blocks() workgroups that count
+ * the words of their uninitialised LDS not holding that pattern (out [blocks], waits). */
+pf_status pf_test_lds_poison(void* stream);
+int32_t pf_test_lds_probe_blocks(void);
+int64_t pf_test_lds_poison_count(void);  /* poison launches the engine's hook has made so far */
+pf_status pf_test_lds_probe(void* stream, int32_t* out);
 /* Live kernel timing for the bench: when on, every pf_run_device records HIP events on
  * the handle's stream right before its first and after its last filter kernel;
  * pf_last_run_ms waits for the last run and returns the device time between them. */

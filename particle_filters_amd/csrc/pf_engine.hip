@@ -614,6 +614,7 @@ pf_status ensure_cov(pf_handle* h) {
 template <typename Real, int NB>
 void launch_cov_part(dim3 grid, const CovParams& c, hipStream_t s) {
   const size_t lds = cov_part_lds<Real, NB>();
+  lds_poison_hook(s);  // tests only (pf_hooks.h)
   hipLaunchKernelGGL((k_cov_part<Real, NB>), grid, dim3(256), lds, s, c);
 }
 
@@ -905,6 +906,53 @@ pf_status dead_filter(pf_handle* h, const std::string& where) {
 }
 
 }  // namespace
+
+namespace pf {
+
+// ---------------------------------------------------------------------------
+// Uninitialised-LDS test hook (pf_hooks.h): k_lds_poison fills a workgroup's whole LDS allocation
+// (160 KB: one workgroup per CU at a time) with 0xFFFFFFFF; 4 workgroups per CU visit every CU.
+// k_lds_probe (test of the mechanism) counts, per workgroup, the words of its uninitialised LDS
+// that do not hold the pattern.
+// ---------------------------------------------------------------------------
+constexpr int PF_LDS_CU_BYTES = 160 * 1024;
+constexpr unsigned PF_LDS_POISON = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(1024) k_lds_poison(unsigned pattern) {
+  extern __shared__ unsigned lds_all[];
+  volatile unsigned* v = lds_all;  // volatile: the stores are the kernel's only effect
+  for (int i = threadIdx.x; i < PF_LDS_CU_BYTES / 4; i += blockDim.x) v[i] = pattern;
+}
+
+__global__ void __launch_bounds__(1024) k_lds_probe(unsigned pattern, int32_t* out) {
+  extern __shared__ unsigned lds_all[];
+  __shared__ int bad;
+  volatile unsigned* v = lds_all;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int i = threadIdx.x; i < PF_LDS_CU_BYTES / 4 - 64; i += blockDim.x) mine += v[i] != pattern;
+  atomicAdd(&bad, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = bad;
+}
+
+static int lds_poison_blocks() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return 4 * (cus > 0 ? cus : 256);
+}
+
+static long long g_lds_poison_count = 0;
+void lds_poison_count_add() { ++g_lds_poison_count; }
+
+void lds_poison(hipStream_t s) {
+  (void)hipFuncSetAttribute((const void*)k_lds_poison, hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS_CU_BYTES);
+  hipLaunchKernelGGL(k_lds_poison, dim3(lds_poison_blocks()), dim3(1024), PF_LDS_CU_BYTES, s, PF_LDS_POISON);
+}
+
+}  // namespace pf
 
 extern "C" {
 
@@ -2099,6 +2147,30 @@ pf_status pf_synchronize(pf_handle* h) {
 }
 
 int32_t pf_last_run_resident(pf_handle* h) { return (h && h->last_resident) ? 1 : 0; }
+
+pf_status pf_test_lds_poison(void* stream) {
+  pf::lds_poison((hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? PF_OK : fail(PF_E_HIP, "k_lds_poison launch failed");
+}
+
+int32_t pf_test_lds_probe_blocks(void) { return pf::lds_poison_blocks(); }
+
+int64_t pf_test_lds_poison_count(void) { return pf::g_lds_poison_count; }
+
+pf_status pf_test_lds_probe(void* stream, int32_t* out) {
+  if (!out) return fail(PF_E_ARG, "pf_test_lds_probe: out is null");
+  const int nb = pf::lds_poison_blocks();
+  int32_t* d = nullptr;
+  if (hipMalloc((void**)&d, nb * sizeof(int32_t)) != hipSuccess) return fail(PF_E_HIP, "pf_test_lds_probe: hipMalloc");
+  (void)hipFuncSetAttribute((const void*)pf::k_lds_probe, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pf::PF_LDS_CU_BYTES - 1024);
+  hipLaunchKernelGGL(pf::k_lds_probe, dim3(nb), dim3(1024), pf::PF_LDS_CU_BYTES - 1024, (hipStream_t)stream,
+                     pf::PF_LDS_POISON, d);
+  hipError_t e = hipMemcpyAsync(out, d, nb * sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  (void)hipFree(d);
+  return e == hipSuccess ? PF_OK : fail(PF_E_HIP, std::string("pf_test_lds_probe: ") + hipGetErrorString(e));
+}
 
 pf_status pf_geometry(pf_handle* h, int32_t* G, int32_t* tile, int32_t* lds) {
   if (!h) return fail(PF_E_ARG, "null handle");

@@ -4,6 +4,8 @@
 #pragma once
 #include <cstdlib>
 
+#include <hip/hip_runtime.h>
+
 namespace pf {
 
 inline bool test_hook(const char* name) {
@@ -11,6 +13,20 @@ inline bool test_hook(const char* name) {
   if (!(on && std::atoi(on) == 1)) return false;
   const char* e = std::getenv(name);
   return e && std::atoi(e) == 1;
+}
+
+// Uninitialised-LDS regression hook (tests/test_gpu_lds_poison.py): with PF_TEST_LDS_POISON=1 (and
+// PF_TEST_HOOKS=1) every launch of the kernels under test is preceded, on its stream, by
+// k_lds_poison, which fills the whole 160 KB of LDS of every CU with 0xFFFFFFFF - a NaN as fp32
+// and as fp64 - so a kernel that reads an LDS word it did not write sees a NaN, not whatever the
+// previous kernel happened to leave (pf_engine.hip).
+void lds_poison(hipStream_t s);
+void lds_poison_count_add();  // launches made by the hook (pf_test_lds_poison_count)
+inline void lds_poison_hook(hipStream_t s) {
+  if (test_hook("PF_TEST_LDS_POISON")) {
+    lds_poison(s);
+    lds_poison_count_add();
+  }
 }
 
 }  // namespace pf

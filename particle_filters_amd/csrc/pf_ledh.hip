@@ -87,13 +87,17 @@ struct LL {
   static hipError_t flow_wave(const FlowParams& p, int grid, hipStream_t s) {
     if constexpr (OK == PF_OBS_ACOUSTIC) {
       // the acoustic h reads the positions only: the flow's algebra in their NX / 2 dimensions
-      // (k_flow_wave_lr); PF_FLOW_LR=0 runs the observation-space kernel (A/B)
-      static const bool lr = !(std::getenv("PF_FLOW_LR") && std::atoi(std::getenv("PF_FLOW_LR")) == 0);
+      // (k_flow_wave_lr); PF_FLOW_LR=0 runs the observation-space kernel (A/B and the test that
+      // compares the two), read per launch
+      const char* lr_env = std::getenv("PF_FLOW_LR");
+      const bool lr = !(lr_env && std::atoi(lr_env) == 0);
       if (lr && p.r_diag) {  // U = R^{-1/2} H8 by a diagonal scaling
+        pf::lds_poison_hook(s);  // tests only (pf_hooks.h)
         hipLaunchKernelGGL((k_flow_wave_lr<NX, NZ, TK>), dim3(grid), dim3(64), 0, s, p);
         return hipGetLastError();
       }
     }
+    pf::lds_poison_hook(s);  // tests only (pf_hooks.h)
     hipLaunchKernelGGL((k_flow_wave<NX, NZ, TK, OK>), dim3(grid), dim3(64), 0, s, p);
     return hipGetLastError();
   }
@@ -139,12 +143,14 @@ struct LL {
   static hipError_t ekf(const double* Pm, const double* x0, const double* P0, const double* Qt, const double* Rt,
                         const double* Z, int64_t T, double* Ps, double* x_out, double* P_out, double* Xp,
                         hipStream_t s) {
+    pf::lds_poison_hook(s);  // tests only (pf_hooks.h)
     hipLaunchKernelGGL((k_ekf_seq<NX, NZ, TK, OK>), dim3(1), dim3(ekf_block<NZ>()), 0, s, Pm, x0, P0, Qt, Rt, Z, T, Ps, x_out, P_out,
                        Xp);
     return hipGetLastError();
   }
   static hipError_t fused(const FusedParams& p, hipStream_t s) {
     if constexpr (OK == PF_OBS_LINEAR) {
+      pf::lds_poison_hook(s);  // tests only (pf_hooks.h)
       hipLaunchKernelGGL((k_ledh_fused<NX, NZ, TK>), dim3(p.nbk), dim3(FusedBlk<NX>::FB), 0, s, p);
       return hipGetLastError();
     } else {

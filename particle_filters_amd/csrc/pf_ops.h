@@ -3,6 +3,7 @@
 // templates for its model family and registers an Ops entry; pf_engine.hip
 // looks the entry up at pf_create time.
 #pragma once
+#include "pf_hooks.h"
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -61,6 +62,7 @@ template <typename Real, int NX, int NZ, int TK, int OK>
 struct Launch {
   static constexpr int BS = StepTraits<Real, NX, NZ, TK, OK>::BS;
   static hipError_t step(const StepParams& p, dim3 grid, size_t smem, hipStream_t s) {
+    lds_poison_hook(s);  // tests only (pf_hooks.h)
     if constexpr (SGrp<NX>::ON) {  // large state: 4 lanes per particle (pf_step_grp.h)
       const bool rd = p.r_diag != 0, ql = p.lq_local != 0 && p.lj_local != 0;
       if (rd && ql) hipLaunchKernelGGL((k_step_grp<Real, NX, NZ, TK, OK, true, true>), grid, dim3(256), smem, s, p);

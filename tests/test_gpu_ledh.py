@@ -288,3 +288,30 @@ def test_fused_run_failure_poisons_handle(monkeypatch):
     st = pf.init_from_gaussian(g["mean0"], g["cov0"])
     res = pf.run(st, Z[:3], tracker="device")
     assert np.all(np.isfinite(res.means))
+
+
+def test_flow_lr_equals_dense_flow(monkeypatch):
+    """Advisor (round 5): the position-space acoustic flow k_flow_wave_lr against the dense
+    observation-space k_flow_wave (PF_FLOW_LR=0, read per launch) on the same inputs - the MAT
+    notebook's joint 16-D / 25-sensor case with the reference's recorded noise: particles, weights,
+    means and the flow's condition numbers step by step to ~1e-9 (both are fp64 evaluations of
+    ledh.py:136-179; they differ only by rounding)."""
+    out = {}
+    for lr in ("1", "0"):
+        monkeypatch.setenv("PF_FLOW_LR", lr)
+        pf, cfg, om, g = make_filter("mat_joint")
+        st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+        sampler = lambda n, nx: cfg.rng.multivariate_normal(np.zeros(nx), om.Q, size=n)  # noqa: E731
+        steps = []
+        for t in range(len(g["Z"])):
+            st = pf.step(st, g["Z"][t], process_noise_sampler=sampler)
+            steps.append((st.particles.copy(), st.weights.copy(), st.mean.copy(), pf.last_resampled,
+                          np.asarray(st.diagnostics["condition_numbers"]).copy()))
+        out[lr] = steps
+    scale = max(1.0, float(np.abs(g["means"]).max()))
+    for t, (a, b) in enumerate(zip(out["1"], out["0"])):
+        assert a[3] == b[3], f"resample decision differs at step {t}"
+        np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-9 * scale, err_msg=f"x t={t}")
+        np.testing.assert_allclose(a[1], b[1], rtol=1e-7, atol=1e-13, err_msg=f"w t={t}")
+        np.testing.assert_allclose(a[2], b[2], rtol=0, atol=1e-9 * scale, err_msg=f"mean t={t}")
+        np.testing.assert_allclose(a[4], b[4], rtol=1e-6, err_msg=f"cond t={t}")

@@ -18,8 +18,8 @@ fp32 rounding bound of the engine's log-weights, computed per particle from the 
 quantities - 2^-21 (1 + |l| + |log-likelihood|) + the fp32 observation and the predicted particle's
 rounding through the likelihood's slopes (sir_philox.c) - a formula, not a measured engine error):
   predicted particles     |dx| <= 2e-6 x scale
-  weights                 total variation <= max(1e-7, eps_w)
-  Neff                    rel <= max(1e-5, 4 eps_w)
+  weights                 total variation <= min(max(1e-7, eps_w), 1e-3)
+  Neff                    rel <= min(max(1e-5, 4 eps_w), 4e-3)
   decision                identical unless Neff is within 1e-3 N of 0.5 N
   ancestors               every slot holds a valid, non-decreasing ancestor; where it differs from
                           searchsorted over the engine's own weights (fp64 cumsum of its fp32
@@ -43,6 +43,8 @@ import time
 
 import numpy as np
 import pytest
+
+from tests import teacher_forced as TF
 
 import bench
 from oracle import sir_philox as SP
@@ -152,7 +154,9 @@ class TraceChain:
         spread = float(np.sum(we[fin] * (np.max(le[fin]) - le[fin].astype(float))))
         band_self = BAND_SELF_ULP * (1.0 + spread)
         sigma = float(np.sqrt(max(c["var_o"], (1e-6 * scale) ** 2)))
-        return dict(scale=scale, tv_bound=max(1e-7, c["eps_w"]), neff_bound=max(1e-5, 4.0 * c["eps_w"]),
+        # the rounding bound, capped by the fixed ceilings of tests/teacher_forced.py (TV 1e-3, Neff 4e-3)
+        return dict(scale=scale, tv_bound=min(max(1e-7, c["eps_w"]), TF.TV_CEILING),
+                    neff_bound=min(max(1e-5, 4.0 * c["eps_w"]), TF.NEFF_CEILING),
                     band_self=band_self, band_oracle=band_self + 2.0 * c["eps_w"],
                     var_rel=c["dvar"] / max(c["var_o"], (1e-6 * scale) ** 2),
                     var_bound=TOL_COV + 4.0 * c["dx_pre"] / sigma)

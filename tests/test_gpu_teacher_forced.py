@@ -10,15 +10,17 @@ the reference's outputs) is started from S_t, and both run step t with identical
 
 Stated tolerances (fp32 engine; ``scale`` = max(1, max |posterior mean|) of the step):
   particles after predict   |dx| <= 2e-6 x scale              (a few fp32 ulps of one step)
-  weights                   total-variation distance <= max(1e-7, eps_w), eps_w the oracle-weighted
+  weights                   total-variation distance <= min(max(1e-7, eps_w), 1e-3), eps_w the oracle-weighted
                             fp32 rounding bound of the engine's log-weights, a formula of the
                             oracle's own quantities (tests/teacher_forced.py docstring: 2^-21 (1 +
                             |log w0| + |log-lik| + the observation / prediction terms) + the
-                            oracle likelihood's change under any particle perturbation within the
-                            2e-6 x scale tolerance above, by its gradient) - never a measured
-                            engine-vs-oracle difference (MAT's 25 sensors at R = 0.01 I give
-                            log-likelihoods of O(1e2-1e4): eps_w grows with them)
-  Neff                      rel <= max(1e-5, 4 eps_w)
+                            oracle likelihood's change under each particle's own state deviation
+                            |x'_e - x'_o| (checked above to be within 2e-6 x scale), by the analytic
+                            gradient - never a measured likelihood difference (MAT's 25 sensors at
+                            R = 0.01 I give log-likelihoods of O(1e2-1e4): eps_w grows with them);
+                            capped at 1e-3 whatever the bound (eps_w_box, the same bound with every
+                            component at the whole 2e-6 x scale box, is kept in the evidence)
+  Neff                      rel <= min(max(1e-5, 4 eps_w), 4e-3)
   decision                  identical unless Neff is within 1e-3 N of 0.5 N
   ancestors                 every post-step slot is an exact copy of one predicted particle; where
                             that ancestor differs from the oracle's, the position lies within
