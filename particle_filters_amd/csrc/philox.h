@@ -122,7 +122,9 @@ __device__ __forceinline__ Normal4<double> normal4<double>(uint64_t seed, uint32
 // fp64 Box-Muller (sincospi, log, sqrt in double) cost ~200 fp64 instructions per 4 normals and
 // was the longest phase of the fused LEDH step's per-particle chain; a normal with 24-bit
 // resolution is a draw of the same N(0, 1) (the reference's own draws come from NumPy's PCG64
-// and are not reproduced bit for bit in device-RNG mode anyway).
+// and are not reproduced bit for bit in device-RNG mode anyway), truncated where the 24-bit
+// uniform bottoms out: |n| <= sqrt(-2 ln 2^-24) = 5.77 sigma (8e-9 of the N(0, 1) mass is never
+// drawn).  tests/test_bm24_normals.py checks moments, tail masses to 5 sigma and the cut.
 __device__ __forceinline__ Normal4<double> normal4_bm24d(uint64_t seed, uint32_t group, uint32_t rep,
                                                          uint32_t epoch, uint32_t stream) {
   const Normal4<float> f = normal4<float>(seed, group, rep, epoch, stream);
