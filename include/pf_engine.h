@@ -210,6 +210,12 @@ pf_status pf_profile_steps(pf_handle* h, const void* dZ, int64_t steps, float* m
  * grid co-resident), 0 if as the launch-per-step loop.  PF_RESIDENT=0 in the
  * environment forces the launch-per-step loop. */
 int32_t pf_last_run_resident(pf_handle* h);
+/* 1 if the last pf_run / pf_run_device ran as the persistent fp64 whole-run kernel (k_persist: one
+ * launch for the T steps, the tail and the statistics; scalar fp64 models, systematic resampling,
+ * grid co-resident; bitwise the launch-per-step loop), 0 otherwise.  Opt-in: PF_PERSIST=1 in the
+ * environment (it is not faster than the launch-per-step loop at N = 1e6).  No reference counterpart
+ * (replaces the per-step calls of models/particle_filter.py:223-269 as the resident kernel does). */
+int32_t pf_last_run_persistent(pf_handle* h);
 /* Uninitialised-LDS test hooks (tests/test_gpu_lds_poison.py; no reference counterpart):
  * pf_test_lds_poison fills the whole 160 KB of LDS of every CU with 0xFFFFFFFF (NaN in fp32 and
  * fp64) on `stream` (a hipStream_t); with PF_TEST_HOOKS=1 and PF_TEST_LDS_POISON=1 in the

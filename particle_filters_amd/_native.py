@@ -132,6 +132,7 @@ SIGNATURES = {
     "pf_profile_steps": (C.c_int32, [_vp, _vp, C.c_int64, C.POINTER(C.c_float)]),
     "pf_geometry": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "pf_last_run_resident": (C.c_int32, [_vp]),
+    "pf_last_run_persistent": (C.c_int32, [_vp]),
     "pf_test_lds_poison": (C.c_int32, [_vp]),
     "pf_test_lds_probe_blocks": (C.c_int32, []),
     "pf_test_lds_poison_count": (C.c_int64, []),

@@ -223,12 +223,18 @@ struct pf_handle {
   struct ResUndo {
     unsigned long long seq;
     uint32_t epoch, ep_res;
-    int crec;
+    int crec, cx, clw;
     unsigned long long hdr;
   };
   std::vector<ResUndo> res_undo;
   int resident_runs = 0;       // diagnostics: pf_run_device calls served by k_resident
   bool last_resident = false;  // the last pf_run_device ran k_resident
+  // persistent fp64 whole-run path (pf_persist.h): granule ring + data flags, tag base, diagnostics
+  unsigned long long* psync = nullptr;
+  size_t psync_words = 0;
+  uint32_t pers_tag = 0;
+  int persist_runs = 0;
+  bool last_persist = false;
   // device-loop covariance for nx > 4 (pf_cov.h): post-resample rows, block partials, sums,
   // per-replicate arrival counters, and the launch geometry
   void* xr = nullptr;        // post-resample rows (with jitter) ...
@@ -683,6 +689,41 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, co
 }
 
 // ---------------------------------------------------------------------------
+// Sync words of the resident and persistent launches (h->rsync): the resident granule ring and
+// hand-off flags, the timeout word, the arrival count (ResParams::arrive / PersistParams::arrive) and
+// the resident entry headers.  Allocated on first use; tags and flag values grow from launch to
+// launch (ResParams::tag0 / flag0), so the words are zeroed only when allocated or when the 32-bit
+// tag space would wrap (rsync_fits false -> rsync_reset).
+size_t rsync_bytes_needed(const pf_handle* h) {
+  const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
+  return (gran_n + 2 * flag_n + 4 + 4 * (size_t)h->R) * sizeof(unsigned long long);
+}
+bool rsync_fits(const pf_handle* h, int64_t T) {
+  const uint64_t tag_span = 4 * (uint64_t)T + 16;
+  return h->rsync && h->rsync_bytes >= rsync_bytes_needed(h) && (uint64_t)h->res_tag + tag_span < 0xFFFFFFFFull;
+}
+pf_status rsync_reset(pf_handle* h) {
+  const size_t bytes = rsync_bytes_needed(h);
+  if (h->rsync_bytes < bytes) {
+    if (h->rsync) HIPCHK(hipFree(h->rsync));
+    h->rsync = nullptr;
+    h->rsync_bytes = 0;
+    HIPCHK(hipMalloc((void**)&h->rsync, bytes));
+    h->rsync_bytes = bytes;
+  }
+  const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
+  const size_t arr_off = gran_n + 2 * flag_n + 2;
+  HIPCHK(hipMemsetAsync(h->rsync, 0, h->rsync_bytes, h->stream));
+  HIPCHK(hipMemsetAsync(h->rsync + arr_off + 1, 0xff, sizeof(unsigned long long), h->stream));
+  h->res_tag = 0;
+  h->res_flag = 0;
+  h->res_arrive = 0;
+  h->res_seq = 0;
+  h->res_hdr = 0;
+  return PF_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Register-resident whole-run path (pf_resident.h).  Used by pf_run_device when
 // the model has a resident kernel (scalar fp32), systematic resampling, the
 // default k_step geometry and a grid that fits co-resident on the device;
@@ -699,33 +740,15 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   if (G > RMAXG || T > (int64_t)0x3fffffff) return PF_OK;
   const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
   const size_t hdr_off = gran_n + 2 * flag_n + 4;  // entry headers [R][4]
-  const size_t bytes = (hdr_off + 4 * (size_t)h->R) * sizeof(unsigned long long);
-  // Tags and flag values grow from launch to launch (ResParams::tag0 / flag0), so the
-  // sync words are zeroed only when allocated or when the 32-bit tag space would wrap.
-  const uint64_t tag_span = 4 * (uint64_t)T + 16;
-  bool zero = false;
-  if (h->rsync_bytes < bytes) {
-    if (h->rsync) HIPCHK(hipFree(h->rsync));
-    h->rsync = nullptr;
-    h->rsync_bytes = 0;
-    HIPCHK(hipMalloc((void**)&h->rsync, bytes));
-    h->rsync_bytes = bytes;
-    zero = true;
-  }
-  if ((uint64_t)h->res_tag + tag_span >= 0xFFFFFFFFull) zero = true;
+  const size_t arr_off = gran_n + 2 * flag_n + 2;  // arrival count, first aborted launch
+  const bool zero = !rsync_fits(h, T);
   if (h->pending) {  // a decision taken before this run is applied first (gather-only launch)
     pf_status st = apply_pending(h, nullptr, nullptr, false);
     if (st) return st;
   }
-  const size_t arr_off = gran_n + 2 * flag_n + 2;  // arrival count, first aborted launch
   if (zero) {
-    HIPCHK(hipMemsetAsync(h->rsync, 0, h->rsync_bytes, h->stream));
-    HIPCHK(hipMemsetAsync(h->rsync + arr_off + 1, 0xff, sizeof(unsigned long long), h->stream));
-    h->res_tag = 0;
-    h->res_flag = 0;
-    h->res_arrive = 0;
-    h->res_seq = 0;
-    h->res_hdr = 0;
+    pf_status st = rsync_reset(h);
+    if (st) return st;
   }
   if (!h->hdr_restore.empty()) {  // a restored checkpoint's entry header, under a fresh id
     const unsigned long long id = ++h->res_run;
@@ -737,7 +760,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     h->hdr_restore.clear();
   }
   if (!h->res_unchecked) h->res_undo.clear();
-  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec, h->res_hdr});
+  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec, h->cx, h->clw, h->res_hdr});
   ResParams q;
   std::memset(&q, 0, sizeof(q));
   q.x_in = (const float*)h->x[h->cx];
@@ -828,7 +851,7 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   if (h->timing && !ext1) HIPCHK(hipEventRecord(h->tev[1], h->stream));
   order.end();
   h->res_hdr = q.hdr_out;  // the state is now what this run's exit header describes
-  h->res_tag += (uint32_t)tag_span;
+  h->res_tag += (uint32_t)(4 * (uint64_t)T + 16);  // the tag span rsync_fits reserves
   h->res_flag += (unsigned long long)T + 1;
   const int k = fo ? 1 : 0;
   h->epoch = q.ep0 + (uint32_t)(2 * T) - k;
@@ -838,6 +861,113 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
   h->res_unchecked = true;
   h->resident_runs++;
   h->last_resident = true;
+  *used = true;
+  return PF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Persistent fp64 whole-run path (pf_persist.h): the launch-per-step loop below, bit for bit, in
+// one launch (its T fused steps, the tail and the finalize), for the scalar fp64 models with
+// systematic resampling, per-workgroup prologues (no k_head), unsharded state and a grid that fits
+// co-resident.  Opt-in (PF_PERSIST=1): at N = 1e6 it measured 25.0 us per step against 23.1 for the
+// launch-per-step loop (same box, profiles/r06/persist): the step is bound by the fp64 Box-Muller /
+// weight chains at 2 waves per SIMD, not by the launch boundary it removes.
+// ---------------------------------------------------------------------------
+pf_status run_persist(pf_handle* h, const void* dZ, const void* dU, int64_t T, int32_t fo, double* dm, double* dc,
+                      double* dn, int32_t* df, double* dl, bool* used) {
+  *used = false;
+  const char* env = std::getenv("PF_PERSIST");
+  if (!(env && std::atoi(env) == 1)) return PF_OK;
+  if (!h->ops->persist || h->res_force_coop || h->method != 0 || h->sharded || use_head(h) || h->lcum_mode || T <= 0 ||
+      T > (int64_t)0x3fffffff || h->tile > 2 * PBS * 4 || h->G > PMAXG)
+    return PF_OK;
+  const int G = h->G, R = h->R;
+  const size_t smem = persist_lds_bytes(G, h->tile);
+  if (smem > 160 * 1024) return PF_OK;
+  const int cap = h->ops->persist_cap ? h->ops->persist_cap(smem) : 0;
+  if ((long long)G * R > (long long)cap) return PF_OK;
+  // the arrival count and timeout word (shared with the resident path), the granule ring and flags
+  if (!rsync_fits(h, T)) {
+    pf_status st = rsync_reset(h);
+    if (st) return st;
+  }
+  const size_t pw = persist_sync_words(R, G);
+  bool zero = (uint64_t)h->pers_tag + (uint64_t)T + 2 >= 0xFFFFFFFFull;
+  if (h->psync_words < pw) {
+    if (h->psync) HIPCHK(hipFree(h->psync));
+    h->psync = nullptr;
+    h->psync_words = 0;
+    HIPCHK(hipMalloc((void**)&h->psync, pw * sizeof(unsigned long long)));
+    h->psync_words = pw;
+    zero = true;
+  }
+  if (zero) {
+    HIPCHK(hipMemsetAsync(h->psync, 0, h->psync_words * sizeof(unsigned long long), h->stream));
+    h->pers_tag = 0;
+  }
+  const size_t gran_n = RCOPIES * gran_copy_stride(R), flag_n = (size_t)R * RMAXG;
+  const size_t arr_off = gran_n + 2 * flag_n + 2;
+  if (!h->res_unchecked) h->res_undo.clear();
+  h->res_undo.push_back({h->res_seq + 1, h->epoch, h->ep_res, h->crec, h->cx, h->clw, h->res_hdr});
+  state_written(h);
+  PersistParams q;
+  std::memset(&q, 0, sizeof(q));
+  q.p = base_params(h);
+  q.p.o_mean = dm;
+  q.p.o_cov = dc;
+  q.p.o_neff = dn;
+  q.p.o_lse = dl;
+  q.p.o_flag = df;
+  for (int k = 0; k < 2; ++k) {
+    q.X[k] = h->x[k];
+    q.L[k] = h->lw[k];
+    q.RB[k] = h->rec[k];
+  }
+  q.cx = h->cx;
+  q.cl = h->clw;
+  q.cr = h->crec;
+  q.z = dZ;
+  q.u = dU;
+  q.T = T;
+  q.fo = fo ? 1 : 0;
+  q.pending = h->pending ? 1 : 0;
+  q.ep0 = h->epoch;
+  q.ep_res0 = h->ep_res;
+  q.gran = h->psync;
+  q.dflag = h->psync + persist_gran_words(R, G);
+  q.tag0 = h->pers_tag;
+  q.arrive = h->rsync + arr_off;
+  q.arrive0 = h->res_arrive;
+  q.seq = ++h->res_seq;
+  q.err = (unsigned int*)(h->rsync + gran_n + 2 * flag_n);
+  GridOrderScope order(h->device, h->stream);
+  if (h->timing) HIPCHK(hipEventRecord(h->tev[0], h->stream));  // stop: stamped by the launch's dispatch
+  const hipError_t e = h->ops->persist(q, G, R, smem, h->stream, h->timing ? h->tev[1] : nullptr);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    h->res_undo.pop_back();
+    --h->res_seq;
+    return PF_OK;  // launch-per-step path
+  }
+  if (e != hipSuccess) return fail(PF_E_HIP, std::string("k_persist launch: ") + hipGetErrorString(e));
+  order.end();
+  h->res_arrive += (unsigned long long)G * R;
+  h->pers_tag += (uint32_t)T + 2;
+  // the buffers the launch-per-step loop would leave current: x flips on every step that predicts or
+  // may gather (and in the tail), the log-weights on every update, the records on every launch
+  const int xflips = (int)((T - ((fo && !h->pending) ? 1 : 0) + 1) & 1);
+  h->cx ^= xflips;
+  h->clw ^= (int)(T & 1);
+  h->crec ^= (int)((T + 1) & 1);
+  const int k = fo ? 1 : 0;
+  h->epoch = q.ep0 + (uint32_t)(2 * T) - k;
+  h->ep_res = h->epoch - 1;
+  h->pending = false;
+  h->lcum_valid = false;
+  h->head_valid = false;
+  h->res_unchecked = true;
+  h->persist_runs++;
+  h->last_persist = true;
   *used = true;
   return PF_OK;
 }
@@ -870,11 +1000,14 @@ pf_status check_resident(pf_handle* h) {
     h->epoch = u->epoch;
     h->ep_res = u->ep_res;
     h->crec = u->crec;
+    h->cx = u->cx;
+    h->clw = u->clw;
     h->res_hdr = u->hdr;
     h->res_undo.clear();
-    h->res_force_coop = true;
+    h->res_force_coop = true;  // resident runs launch cooperatively, persistent ones not at all
     h->last_resident = false;
-    return fail(PF_E_RETRY, "k_resident: the grid was not co-resident (other work on the GPU); nothing was "
+    h->last_persist = false;
+    return fail(PF_E_RETRY, "k_resident / k_persist: the grid was not co-resident (other work on the GPU); nothing was "
                             "computed, the state is unchanged and the next run launches cooperatively");
   }
   // The launch wrote its particles and records in place: the state is unusable.  Poison
@@ -1179,6 +1312,7 @@ void pf_destroy(pf_handle* h) {
     if (h->rec[k]) (void)hipFree(h->rec[k]);
   }
   if (h->rsync) (void)hipFree(h->rsync);
+  if (h->psync) (void)hipFree(h->psync);
   for (hipEvent_t e : h->tev)
     if (e) (void)hipEventDestroy(e);
   if (h->head) (void)hipFree(h->head);
@@ -1393,6 +1527,13 @@ pf_status pf_run_device(pf_handle* h, const void* dZ, const void* dU, int64_t T,
     h->last_resident = false;
     pf_status st = run_resident(h, dZ, dU, T, first_update_only, d_means, (h->nx <= 4) ? d_covs : nullptr, d_neff,
                                 d_flags, d_lse, &used);
+    if (st || used) return st;
+  }
+  {
+    bool used = false;
+    h->last_persist = false;
+    pf_status st = run_persist(h, dZ, dU, T, first_update_only, d_means, (h->nx <= 4) ? d_covs : nullptr, d_neff,
+                               d_flags, d_lse, &used);
     if (st || used) return st;
   }
   const int R = h->R;
@@ -2147,6 +2288,7 @@ pf_status pf_synchronize(pf_handle* h) {
 }
 
 int32_t pf_last_run_resident(pf_handle* h) { return (h && h->last_resident) ? 1 : 0; }
+int32_t pf_last_run_persistent(pf_handle* h) { return (h && h->last_persist) ? 1 : 0; }
 
 pf_status pf_test_lds_poison(void* stream) {
   pf::lds_poison((hipStream_t)stream);

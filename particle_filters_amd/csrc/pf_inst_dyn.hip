@@ -84,6 +84,8 @@ struct DynLaunch {
     o.prepare = &prepare;
     o.resident = nullptr;
     o.resident_cap = nullptr;
+    o.persist = nullptr;
+    o.persist_cap = nullptr;
     o.shard_offspring = &shard_offspring;
     o.shard_adopt = &shard_adopt;
     return o;

@@ -324,24 +324,17 @@ struct Head {
 // contiguous records [t*RPT, t*RPT + RPT).  Max first, then per-record factors,
 // then plain sums: a short dependency chain with one parallel exp per record.
 // ---------------------------------------------------------------------------
+// The summary from the record heads already in registers (thread t: records [t RPT, t RPT + RPT),
+// -inf / 0 past G) and the uniform flag: prologue() after its loads, and the persistent fp64 step
+// (pf_persist.h), which reads the heads from its record granules - the same arithmetic, bit for bit.
 template <int NX, int BS>
-__device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, double thresh, bool allow, bool force,
-                                         bool want_prefix, double* red, double* Pl) {
-  using RC = Rec<NX>;
+__device__ __forceinline__ Head prologue_reduce(const double (&mk)[MAXG / BS], const double (&s0k)[MAXG / BS],
+                                                const double (&s00k)[MAXG / BS], double uni, int G, int64_t N,
+                                                double thresh, bool allow, bool force, bool want_prefix, double* red,
+                                                double* Pl) {
   constexpr int RPT = MAXG / BS;  // records per thread
   const int t = threadIdx.x;
   const int k0 = t * RPT;
-  // one round of loads: the uniform flag and this thread's record heads
-  double mk[RPT], s0k[RPT], s00k[RPT];
-  const double uni = rec[RC::UNI * G];
-#pragma unroll
-  for (int j = 0; j < RPT; ++j) {
-    const int k = k0 + j;
-    const bool in = k < G;
-    mk[j] = in ? rec[RC::M * G + k] : -INFINITY;
-    s0k[j] = in ? rec[RC::S0 * G + k] : 0.0;
-    s00k[j] = in ? rec[RC::S00 * G + k] : 0.0;
-  }
   Head h;
   h.uniform = uni != 0.0;  // a launch-wide property
   h.resample = 0;
@@ -388,6 +381,26 @@ __device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, do
   return h;
 }
 
+template <int NX, int BS>
+__device__ __forceinline__ Head prologue(const double* rec, int G, int64_t N, double thresh, bool allow, bool force,
+                                         bool want_prefix, double* red, double* Pl) {
+  using RC = Rec<NX>;
+  constexpr int RPT = MAXG / BS;  // records per thread
+  const int k0 = threadIdx.x * RPT;
+  // one round of loads: the uniform flag and this thread's record heads
+  double mk[RPT], s0k[RPT], s00k[RPT];
+  const double uni = rec[RC::UNI * G];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int k = k0 + j;
+    const bool in = k < G;
+    mk[j] = in ? rec[RC::M * G + k] : -INFINITY;
+    s0k[j] = in ? rec[RC::S0 * G + k] : 0.0;
+    s00k[j] = in ? rec[RC::S00 * G + k] : 0.0;
+  }
+  return prologue_reduce<NX, BS>(mk, s0k, s00k, uni, G, N, thresh, allow, force, want_prefix, red, Pl);
+}
+
 // Head of a replicate as k_head stored it (same fields prologue() returns; the
 // prefix Pl[0..G] staged into LDS when this kernel searches it).  want_prefix must
 // be what the caller's own prologue call would have passed.
@@ -417,17 +430,18 @@ __device__ __forceinline__ Head load_head(const double* head, int r, int G, bool
 // log normaliser, decision (out_step) and the uniform-weight mean/cov of freshly
 // resampled particles (out_post_step).  Field f of the output vector is reduced
 // by workgroup f mod nblk (spreads the work when NX is large).
-template <int NX, int BS>
-__device__ void write_outputs(const StepParams& p, const double* rec, const Head& h, int r, int R, int blk, int nblk,
-                              double* red) {
+// rec(f, k): field f of tile k's record (plain memory, or the persistent step's granules)
+template <int NX, int BS, class RecF>
+__device__ void write_outputs_f(const StepParams& p, int64_t out_step, int64_t out_post_step, RecF&& rec_at,
+                                const Head& h, int r, int R, int blk, int nblk, double* red) {
   using RC = Rec<NX>;
   const int t = threadIdx.x;
   const int G = p.G;
-  const bool pre = p.out_step >= 0 && !h.uniform;
-  const bool want_post = p.out_post_step >= 0;
+  const bool pre = out_step >= 0 && !h.uniform;
+  const bool want_post = out_post_step >= 0;
   if (!pre && !want_post) return;
   if (pre && blk == 0 && t == 0) {
-    const int64_t o = p.out_step * R + r;
+    const int64_t o = out_step * R + r;
     p.o_neff[o] = h.neff;
     p.o_lse[o] = h.lse;
     p.o_flag[o] = h.resample;
@@ -440,17 +454,17 @@ __device__ void write_outputs(const StepParams& p, const double* rec, const Head
     for (int f = 0; f < 2 * NF + 1; ++f) v[f] = 0.0;
     for (int k = t; k < G; k += BS) {
       if (pre) {
-        const double s0 = rec[RC::S0 * G + k];
+        const double s0 = rec_at(RC::S0, k);
         if (s0 > 0.0) {
-          const double fk = exp(rec[RC::M * G + k] - h.M);
+          const double fk = exp(rec_at(RC::M, k) - h.M);
 #pragma unroll
-          for (int f = 0; f < NF; ++f) v[f] += rec[(RC::S1 + f) * G + k] * fk;
+          for (int f = 0; f < NF; ++f) v[f] += rec_at(RC::S1 + f, k) * fk;
         }
       }
       if (want_post) {
-        v[2 * NF] += rec[RC::CNT * G + k];
+        v[2 * NF] += rec_at(RC::CNT, k);
 #pragma unroll
-        for (int f = 0; f < NF; ++f) v[NF + f] += rec[(RC::A1 + f) * G + k];
+        for (int f = 0; f < NF; ++f) v[NF + f] += rec_at(RC::A1 + f, k);
       }
     }
     block_sum_k<2 * NF + 1, BS>(v, red);
@@ -458,7 +472,7 @@ __device__ void write_outputs(const StepParams& p, const double* rec, const Head
     const double cnt = v[2 * NF];
     for (int pass = 0; pass < 2; ++pass) {
       if (pass == 0 ? !pre : !(want_post && cnt > 0.0)) continue;
-      const int64_t o = (pass == 0 ? p.out_step : p.out_post_step) * R + r;
+      const int64_t o = (pass == 0 ? out_step : out_post_step) * R + r;
       const double* m = v + pass * NF;
       const double den = pass == 0 ? h.S : cnt;
       for (int d = 0; d < NX; ++d) p.o_mean[o * NX + d] = m[d] / den;
@@ -476,7 +490,7 @@ __device__ void write_outputs(const StepParams& p, const double* rec, const Head
     if (blk >= 2 * NX) return;  // no field of this workgroup (field f is reduced by workgroup f mod nblk)
     double cnt = 0.0;
     if (want_post) {
-      for (int k = t; k < G; k += BS) cnt += rec[RC::CNT * G + k];
+      for (int k = t; k < G; k += BS) cnt += rec_at(RC::CNT, k);
       cnt = block_sum<BS>(cnt, red);
     }
     const bool post = want_post && cnt > 0.0;
@@ -487,19 +501,27 @@ __device__ void write_outputs(const StepParams& p, const double* rec, const Head
       double acc = 0.0;
       for (int k = t; k < G; k += BS) {
         if (is_post) {
-          acc += rec[(RC::A1 + d) * G + k];
+          acc += rec_at(RC::A1 + d, k);
         } else {
-          const double s0 = rec[RC::S0 * G + k];
-          if (s0 > 0.0) acc += rec[(RC::S1 + d) * G + k] * exp(rec[RC::M * G + k] - h.M);
+          const double s0 = rec_at(RC::S0, k);
+          if (s0 > 0.0) acc += rec_at(RC::S1 + d, k) * exp(rec_at(RC::M, k) - h.M);
         }
       }
       acc = block_sum<BS>(acc, red);
       if (t == 0) {
-        const int64_t o = (is_post ? p.out_post_step : p.out_step) * R + r;
+        const int64_t o = (is_post ? out_post_step : out_step) * R + r;
         p.o_mean[o * NX + d] = acc / (is_post ? cnt : h.S);
       }
     }
   }
+}
+
+template <int NX, int BS>
+__device__ void write_outputs(const StepParams& p, const double* rec, const Head& h, int r, int R, int blk, int nblk,
+                              double* red) {
+  const int G = p.G;
+  write_outputs_f<NX, BS>(p, p.out_step, p.out_post_step, [rec, G](int f, int k) { return rec[f * G + k]; }, h, r, R, blk,
+                          nblk, red);
 }
 
 // Global CDF values of input tile k, in LDS:

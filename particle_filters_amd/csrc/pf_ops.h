@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "pf_kernels.h"
+#include "pf_persist.h"
 #include "pf_resident.h"
 #include "pf_shard_kernels.h"
 #include "pf_step_grp.h"
@@ -45,6 +46,11 @@ struct Ops {
   hipError_t (*stream)(const StepParams&, int R, size_t smem, hipStream_t);
   int (*resident_cap)(bool trace);  // workgroups of k_resident (the trace instance when trace) co-resident
                                     // on the current device (0: unknown)
+  // persistent whole-run kernel of the scalar fp64 models (pf_persist.h; null otherwise): a plain
+  // launch of the G x R grid (hipErrorCooperativeLaunchTooLarge when it exceeds persist_cap); ev1: the
+  // launch's own stop timestamp (null: none)
+  hipError_t (*persist)(const PersistParams&, int G, int R, size_t smem, hipStream_t, hipEvent_t ev1);
+  int (*persist_cap)(size_t smem);  // co-resident workgroups of k_persist with smem bytes of LDS
   // within-filter sharding (pf_shard_kernels.h)
   hipError_t (*shard_offspring)(const void* x, int64_t N, int64_t Npad, const double* cdf, double U, double lo,
                                 double mass, int64_t Ntot, int64_t a, int64_t n, void* out, hipStream_t, int nx);
@@ -141,6 +147,8 @@ struct Launch {
     o.resident = nullptr;
     o.resident_cap = nullptr;
     o.stream = nullptr;
+    o.persist = nullptr;
+    o.persist_cap = nullptr;
     o.shard_offspring = &shard_offspring;
     o.shard_adopt = &shard_adopt;
     return o;
@@ -238,6 +246,42 @@ struct StreamLaunch {
 };
 
 template <int NX, int NZ, int TK, int OK>
+struct PersistLaunch {
+  // Every workgroup waits for the others' records, so the grid must be co-resident: a plain launch
+  // after the check against the occupancy API (the kernel checks it again itself: res_arrive)
+  static hipError_t launch(const PersistParams& p, int G, int R, size_t smem, hipStream_t s, hipEvent_t ev1) {
+    lds_poison_hook(s);  // tests only (pf_hooks.h)
+    if ((long long)G * R > (long long)cap(smem)) return hipErrorCooperativeLaunchTooLarge;
+    PersistParams q = p;
+    void* args[] = {&q};
+    return hipExtLaunchKernel((const void*)k_persist<double, NX, NZ, TK, OK>, dim3(G, R), dim3(PBS), args, smem, s,
+                              nullptr, ev1, 0);
+  }
+  // CUs x workgroups per CU from the occupancy API, cached per device and LDS size
+  static int cap(size_t smem) {
+    static thread_local int cached_dev = -1, cached_cap = 0;  // per thread: no shared mutable state
+    static thread_local size_t cached_smem = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev != cached_dev || smem != cached_smem) {
+      const void* fn = (const void*)k_persist<double, NX, NZ, TK, OK>;
+      int cus = 0, per_cu = 0;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess) {
+        (void)hipGetLastError();  // (not sticky for the launches that follow)
+        return 0;
+      }
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, PBS, smem) != hipSuccess)
+        return 0;
+      cached_dev = dev;
+      cached_smem = smem;
+      cached_cap = cus * per_cu;
+    }
+    return cached_cap;
+  }
+};
+
+template <int NX, int NZ, int TK, int OK>
 inline void register_both() {
   Ops f32 = Launch<float, NX, NZ, TK, OK>::make(PF_PRECISION_FP32);
   if constexpr (NX == 1) {
@@ -246,7 +290,12 @@ inline void register_both() {
     f32.stream = &StreamLaunch<NZ, TK, OK>::launch;
   }
   register_ops(f32);
-  register_ops(Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64));
+  Ops f64 = Launch<double, NX, NZ, TK, OK>::make(PF_PRECISION_FP64);
+  if constexpr (NX == 1) {
+    f64.persist = &PersistLaunch<NX, NZ, TK, OK>::launch;
+    f64.persist_cap = &PersistLaunch<NX, NZ, TK, OK>::cap;
+  }
+  register_ops(f64);
 }
 
 }  // namespace pf
