@@ -632,6 +632,12 @@ __device__ __forceinline__ int sys_count_below(double x, double U, int N) {
   return sys_count_exact(x, U, N, c);
 }
 
+template <typename Real>
+__device__ __forceinline__ Real rmax(Real a, Real b) {
+  if constexpr (sizeof(Real) == 4) return fmaxf(a, b);
+  else return fmax(a, b);
+}
+
 // block maximum of floats (every thread gets it); redf >= BS / 64 floats, free on entry
 template <int BS>
 __device__ __forceinline__ float block_max_f(float v, float* redf) {
@@ -643,6 +649,13 @@ __device__ __forceinline__ float block_max_f(float v, float* redf) {
 #pragma unroll
   for (int i = 1; i < NW; ++i) M = fmaxf(M, redf[i]);
   return M;
+}
+
+// block maximum in the engine precision (fp32: block_max_f on the staging floats; fp64: block_max)
+template <int BS, typename Real>
+__device__ __forceinline__ Real block_max_r(Real v, double* stage) {
+  if constexpr (sizeof(Real) == 4) return block_max_f<BS>(v, (float*)stage);
+  else return block_max<BS>(v, stage);
 }
 
 // exclusive block max-scan of ints (-1 below thread 0); redi >= BS / 64 ints
@@ -962,6 +975,18 @@ struct WAcc {
     for (int i = 0; i < NS; ++i) out[1 + i] = wave_sum_ud(acc[i]);
     out[0] = Mw;
   }
+  // Merge of add_ref8 sums in fp64 (fp64 engine: every thread's sums share the workgroup maximum, so the
+  // record is their plain block sum; out[0..NS] in every thread)
+  template <int BS>
+  __device__ __forceinline__ void block_sum_ref(double* red, double* out) {
+    double v[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) v[i] = (double)s[i];
+    block_sum_k<NS, BS>(v, red);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) out[1 + i] = v[i];
+    out[0] = m;
+  }
   // Merge of add_ref8 sums (one reference M for the whole workgroup): the partials staged in LDS,
   // wave 0 sums them in fp64 (lane l: threads l, l + 64, ...), then one DPP sum per field.
   template <int BS>
@@ -1023,8 +1048,16 @@ __host__ __device__ constexpr int lds_tile(int G) { return LDS_PL + ((G + 8) & ~
 #ifndef PF_STEP_WPE
 #define PF_STEP_WPE 4
 #endif
+// fp64 scalar state: >= 2 waves per SIMD (its 170 VGPRs; capped at 168 for 3 waves it spills 144 B per
+// lane and runs 23.5 instead of 21.0 us/step, profiles/r06/fp64): 512 workgroups resident, config 2's
+// 489 tiles of 2048 particles in one round
+#ifndef PF_STEP_WPE_D
+#define PF_STEP_WPE_D 2
+#endif
+template <typename Real, int NX>
+constexpr int step_wpe = NX == 1 ? (sizeof(Real) == 4 ? PF_STEP_WPE : PF_STEP_WPE_D) : 1;
 template <typename Real, int NX, int NZ, int TK, int OK>
-__global__ void __launch_bounds__(step_bs<NX>) __attribute__((amdgpu_waves_per_eu((NX == 1 && sizeof(Real) == 4) ? PF_STEP_WPE : 1)))
+__global__ void __launch_bounds__(step_bs<NX>) __attribute__((amdgpu_waves_per_eu(step_wpe<Real, NX>)))
 k_step(StepParams p) {
   using M = Model<Real, NX, NZ, TK, OK>;
   using RC = Rec<NX>;
@@ -1072,7 +1105,16 @@ k_step(StepParams p) {
 #define PF_STEP_FAST 1
 #endif
   constexpr bool FAST2 = PF_STEP_FAST && NX == 1 && CH == 4 && sizeof(Real) == 4;
-  constexpr int QC = FAST2 ? 4 : 1;
+  // fp64 scalar state (the reference's precision, BASELINE config 2's fp64 line): the same straight-
+  // line finish - both chunks speculated under the prologue, one exponential per slot against the
+  // workgroup maximum (add_ref8) instead of the online max (up to two per slot, lane-divergent), the
+  // record's sums merged as plain fp64 sums
+#ifndef PF_STEP_FAST_D
+#define PF_STEP_FAST_D 1
+#endif
+  constexpr bool FASTD = PF_STEP_FAST_D && NX == 1 && CH == 4 && sizeof(Real) == 8;
+  constexpr bool FASTX = FAST2 || FASTD;
+  constexpr int QC = FASTX ? 4 : 1;
   Real qx[QC], qll[QC];
   bool spec1 = false;  // qx / qll hold the second chunk's predicted particles and log-likelihoods
   Real z[NZ];
@@ -1126,7 +1168,7 @@ k_step(StepParams p) {
           sll[e] = (p.do_update == 1) ? M::loglik(sx[e], z, P, p.r_diag != 0) : Real(0);
         }
       }
-      if constexpr (FAST2) {
+      if constexpr (FASTX) {
         if (pre1 && p.do_update == 1) {
           const int64_t i1 = o0 + (int64_t)(t + BS) * CH;
           Real n4[4];
@@ -1347,13 +1389,13 @@ k_step(StepParams p) {
     // thread's 8 gathered slots straight through, weighed against the workgroup maximum as the fast
     // path does - so this step and the same step run as a gather-only launch followed by a fast launch
     // (a run cut at a resample) give bitwise the same records
-    if constexpr (FAST2) {
+    if constexpr (FASTX) {
 #ifndef PF_GFAST
 #define PF_GFAST 1
 #endif
       gfast = PF_GFAST && gather && p.do_predict && p.do_update == 1 && nchunks <= 2 * BS;
       Real xv[8], lp[8];
-      float mt = -INFINITY;  // this thread's maximum log-weight
+      Real mt = -INFINITY;  // this thread's maximum log-weight
       if (gfast && t < nchunks) {
         const int ca = t, cb = t + BS;
         const int64_t ia = o0 + (int64_t)ca * CH, ib = o0 + (int64_t)cb * CH;
@@ -1403,7 +1445,7 @@ k_step(StepParams p) {
           lp[e] = in ? lu + M::loglik(xe, z, P, p.r_diag != 0) : -INFINITY;
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) mt = fmaxf(mt, lp[e]);
+        for (int e = 0; e < 8; ++e) mt = rmax<Real>(mt, lp[e]);
         if (na == 4) {
           store4<Real>(x_out + ia, xv);
           store4<Real>(lw_out + ia, lp);
@@ -1424,7 +1466,7 @@ k_step(StepParams p) {
         }
       }
       if (gfast) {  // uniform: the workgroup's reference maximum, then the thread's sums against it
-        const float Mb = block_max_f<BS>(mt, (float*)(cdf + 32));  // the merge staging area: free here
+        const Real Mb = block_max_r<BS>(mt, cdf + 32);  // the merge staging area: free here
         if (t < nchunks) acc.add_ref8(lp, xv, Mb);
       }
     }
@@ -1433,7 +1475,7 @@ k_step(StepParams p) {
     PF_STAMP(3);
     // fast finish of the fp32 scalar step (uniform per workgroup): every chunk of the thread was
     // speculated and nothing is gathered
-    if constexpr (FAST2) {
+    if constexpr (FASTX) {
 #ifndef PF_NO_PRE1
       constexpr int SPEC_CHUNKS = 2;
 #else
@@ -1441,7 +1483,7 @@ k_step(StepParams p) {
 #endif
       fast = !gather && p.do_update == 1 && nchunks <= SPEC_CHUNKS * BS;  // fused step, or update only
       Real lp[8], xv[8];
-      float mt = -INFINITY;  // this thread's maximum log-weight
+      Real mt = -INFINITY;  // this thread's maximum log-weight
       if (fast && t < nchunks) {
         const Real lu = (Real)lprev_uniform;
         const int64_t ia = o0 + (int64_t)t * CH, ib = o0 + (int64_t)(t + BS) * CH;
@@ -1459,7 +1501,7 @@ k_step(StepParams p) {
         // makes, so a step after a gather-only launch (a run cut at a resample) and the same step fused
         // with its gather give bitwise the same records: a run cut into segments stays the uninterrupted run
 #pragma unroll
-        for (int e = 0; e < 8; ++e) mt = fmaxf(mt, lp[e]);
+        for (int e = 0; e < 8; ++e) mt = rmax<Real>(mt, lp[e]);
         if (na == 4) {
           if (write_x) store4<Real>(x_out + ia, xv);
           store4<Real>(lw_out + ia, lp);
@@ -1480,7 +1522,7 @@ k_step(StepParams p) {
         }
       }
       if (fast) {  // uniform
-        const float Mb = block_max_f<BS>(mt, (float*)(cdf + 32));  // the merge staging area: free here
+        const Real Mb = block_max_r<BS>(mt, cdf + 32);  // the merge staging area: free here
         if (t < nchunks) acc.add_ref8(lp, xv, Mb);
       }
     }
@@ -1504,6 +1546,10 @@ k_step(StepParams p) {
     }
     else
 #endif
+    if constexpr (FASTD) {
+      if (fast || gfast) acc.template block_sum_ref<BS>(red, w);  // one reference maximum: plain sums
+      else acc.template block_merge<BS>(red, w);
+    } else
       acc.template block_merge<BS>(red, w);
     if (t == 0) {
       fin[RC::M] = w[0];

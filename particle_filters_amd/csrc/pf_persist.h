@@ -365,23 +365,18 @@ __global__ void __launch_bounds__(PBS) __attribute__((amdgpu_waves_per_eu(2))) k
         }
       }
     };
+    // k_step's fast finishes (FASTD): one reference maximum for the workgroup, one exponential per slot
+    const bool ref_merge = upd && (!gather || pred);
     if (!gather) {
-      // ---- (N) no resample: the weight shift of the speculated slots (k_step's chunk loop) ------
+      // ---- (N) no resample: the weight shift of the speculated slots (k_step's fast finish) -----
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int nv = nv_of(c);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          xv[4 * c + e] = e < nv ? SX(c, e) : Real(0);  // slots past the tile: a finite placeholder
-          lp[4 * c + e] = h.uniform ? lu : SL(c, e) - lse_r;
-        }
-        if (upd) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (e >= nv) break;
-            lp[4 * c + e] = lp[4 * c + e] + SLL(c, e);
-            acc.add(lp[4 * c + e], &xv[4 * c + e]);
-          }
+          const Real v = (h.uniform ? lu : SL(c, e) - lse_r) + SLL(c, e);
+          xv[4 * c + e] = e < nv ? SX(c, e) : Real(0);  // slots past the tile: zero weight, finite value
+          lp[4 * c + e] = (upd && e < nv) ? v : -INFINITY;
         }
         store_chunk(c);
       }
@@ -438,7 +433,7 @@ __global__ void __launch_bounds__(PBS) __attribute__((amdgpu_waves_per_eu(2))) k
           const Real ll = upd ? M::loglik(xe, z, P, p.r_diag != 0) : Real(0);
           if (upd) {
             lq[e] = lq[e] + ll;
-            acc.add(lq[e], xe);
+            if (!ref_merge) acc.add(lq[e], xe);  // (k_step's generic gather loop)
           }
           x[e] = xe[0];
         }
@@ -446,12 +441,13 @@ __global__ void __launch_bounds__(PBS) __attribute__((amdgpu_waves_per_eu(2))) k
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const Real xo = e < nv ? x[e] : Real(0);
+          const Real lo = e < nv ? lq[e] : -INFINITY;
           if (c == 0) {
             xv[e] = xo;
-            lp[e] = lq[e];
+            lp[e] = lo;
           } else {
             xv[4 + e] = xo;
-            lp[4 + e] = lq[e];
+            lp[4 + e] = lo;
           }
         }
         if (c == 0) store_chunk(0);
@@ -460,11 +456,19 @@ __global__ void __launch_bounds__(PBS) __attribute__((amdgpu_waves_per_eu(2))) k
     }
 
     PX_MARK(4);
+    if (ref_merge) {  // the workgroup maximum, then every thread's sums against it (add_ref8)
+      Real mt = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mt = rmax<Real>(mt, lp[e]);
+      const Real Mb = block_max<BS>(mt, red);
+      if (tix < nchunks) acc.add_ref8(lp, xv, Mb);
+    }
     // ---- (R) the tile record (k_step's merge), stored and published ---------------------------
     __syncthreads();  // all tile-CDF / ancestor / Mk reads are done
     if (upd) {
       double w[1 + WA::NS];
-      acc.template block_merge<BS>(red, w);
+      if (ref_merge) acc.template block_sum_ref<BS>(red, w);
+      else acc.template block_merge<BS>(red, w);
       if (t == 0) {
         fin[RC::M] = w[0];
         fin[RC::S0] = w[1];
