@@ -14,6 +14,13 @@ inline bool test_hook(const char* name) {
   const char* e = std::getenv(name);
   return e && std::atoi(e) == 1;
 }
+// the integer value of a test hook variable (0 unless PF_TEST_HOOKS=1)
+inline int test_hook_int(const char* name) {
+  const char* on = std::getenv("PF_TEST_HOOKS");
+  if (!(on && std::atoi(on) == 1)) return 0;
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
+}
 
 // Uninitialised-LDS regression hook (tests/test_gpu_lds_poison.py): with PF_TEST_LDS_POISON=1 (and
 // PF_TEST_HOOKS=1) every launch of the kernels under test is preceded, on its stream, by

@@ -93,7 +93,9 @@ struct LL {
       const bool lr = !(lr_env && std::atoi(lr_env) == 0);
       if (lr && p.r_diag) {  // U = R^{-1/2} H8 by a diagonal scaling
         pf::lds_poison_hook(s);  // tests only (pf_hooks.h)
-        hipLaunchKernelGGL((k_flow_wave_lr<NX, NZ, TK>), dim3(grid), dim3(64), 0, s, p);
+        FlowParams q = p;
+        q.lr_force = pf::test_hook_int("PF_TEST_FLOW_LR_FORCE");  // tests only (pf_hooks.h)
+        hipLaunchKernelGGL((k_flow_wave_lr<NX, NZ, TK>), dim3(grid), dim3(64), 0, s, q);
         return hipGetLastError();
       }
     }

@@ -145,6 +145,10 @@ struct FlowParams {
   const double* xbar;
   int64_t xbar_stride, u_stride;
   int integ;
+  // test hook (pf_hooks.h, PF_TEST_FLOW_LR_FORCE): k_flow_wave_lr's fallbacks forced - bit 0 the
+  // Householder QR instead of the Gram's Cholesky factor, bit 1 the separate pivoted determinants,
+  // bit 2 the +1e-12 I retry; 0 in every product launch
+  int lr_force;
 };
 
 // ---------------------------------------------------------------------------
@@ -1179,23 +1183,30 @@ __global__ void __launch_bounds__(64) k_flow_wave(FlowParams p) {
 //
 // The acoustic h reads the positions only, so H = H8 E with E the NR x NX position selection and
 // H8 = dh/d(positions) (NZ x NR, NR = 8 for the joint 4-target model against NZ = 25 sensors).  With
-// R diagonal, U = R^{-1/2} H8 = Q Rq (thin Householder QR over the wave: lane k holds row k) and
+// R diagonal, U = R^{-1/2} H8 and Rq the NR x NR upper-triangular factor with Rq^T Rq = U^T U (= W, the
+// Gram): the Cholesky factor of W, W formed on the fp64 matrix cores; where W is not numerically
+// positive definite (a pivot below 1e-12 of its diagonal) the thin Householder QR U = Q Rq over the
+// wave instead (lane k holds row k; the fallback, FlowParams::lr_force bit 0 forces it in tests), and
 //   H8^T S^{-1} H8 = Rq^T D^{-1} Rq,  D = I + lam Rq P_pp Rq^T   (NR x NR, symmetric, eigenvalues >= 1)
 // (S = R^{1/2} (I + lam U P_pp U^T) R^{1/2}; Q^T (I + Q M Q^T)^{-1} Q = (I + M)^{-1}), so
 //   A v  = -1/2 P H^T S^{-1} H v = G v_pos,  G = -1/2 P_{:,pos} Rq^T D^{-1} Rq          (NX x NR)
 //   c    = P H^T R^{-1}(z - e) = P_{:,pos} H8^T R^{-1} (z - e)
 //   det(I + dlam A) = det(S - dlam/2 M) / det(S) = det(I + c1 Rq P_pp Rq^T) / det(D),  c1 = lam - dlam/2
 // (Sylvester; the reference's +1e-12 I retry is flow_logdet's c2 = lam - dlam / (2 (1 + eps)) form).
-// Per pseudo-time step the dense algebra is NR x NR: the QR (sensor rows mirrored in both half-waves,
-// each half summing half of a reflector's reductions), M = Rq P_pp Rq^T as two fp64 MFMA products,
+// Per pseudo-time step the dense algebra is NR x NR: the Gram and its Cholesky factor (or the QR:
+// sensor rows mirrored in both half-waves, each half summing half of a reflector's reductions),
+// M = Rq P_pp Rq^T as two fp64 MFMA products,
 // and one Gauss-Jordan elimination of [D | Rq | C] in registers (column per lane, pivot columns by
 // DPP row_newbcast) that gives D^{-1} Rq and both determinants; the flow update then runs in the
 // position space (K = -1/2 Rq^T D^{-1} Rq, 8-vectors between lanes by readlane) - instead of
-// k_flow_wave's NZ x 2NZ Gauss-Jordan through LDS.  The QR keeps the algebra as accurate as the
-// reference's S solve: a Woodbury form through W = H8^T R^{-1} H8 squares the condition of H8 (W spans
-// 1e-4 .. 4e5 next to a sensor) and lost 2e-4 of the flow; with the QR, a 40-digit recomputation of
-// the MAT golden's most ill-conditioned particle (cond S = 5e6) puts this algebra at 3.3e-9 of the
-// exact flow and the reference's own fp64 path at 3.1e-8 (tools/flow_accuracy.py).  The flow's
+// k_flow_wave's NZ x 2NZ Gauss-Jordan through LDS.  A Woodbury form solving with W itself squares
+// the condition of H8 (W spans 1e-4 .. 4e5 next to a sensor) and lost 2e-4 of the flow; the factor
+// Rq does not (only Rq^T D^{-1} Rq enters the flow, D's eigenvalues are >= 1): a 40-digit
+// recomputation of the MAT golden's most ill-conditioned particle (cond S = 5e6) puts this algebra at
+// 2.4e-9 of the exact flow and the reference's own fp64 path at 3.1e-8 (tools/flow_accuracy.py).  The
+// determinant pair comes from the one Gauss-Jordan (lr_gj_pair); when a sign there is not positive,
+// separate pivoted eliminations (lr_logdet) and then the reference's +1e-12 I retry (FlowParams::
+// lr_force bits 1 and 2 force those paths in tests).  The flow's
 // reciprocals (Jacobian rows, reflector scales, pivots) are v_rcp_f64 + two Newton steps (within an
 // ulp of the division); h and the weight terms evaluate as in k_flow_wave (identical expressions).
 // Diagonal R only (the host takes k_flow_wave otherwise).
@@ -1640,7 +1651,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
         for (int r = 0; r < NR; ++r) wa[r] = sm[SM::WC + cw * NR + r];
         bool okc = true;
         lr_chol_pivot<NR, 0>(wa, rr, sm[SM::WC + cw * NR + cw], okc, r16);  // dg: W(c, c)
-        if (__builtin_amdgcn_readlane(okc ? 1 : 0, 0)) {
+        if (!(p.lr_force & 1) && __builtin_amdgcn_readlane(okc ? 1 : 0, 0)) {
           if (t < NR)
 #pragma unroll
             for (int pr = 0; pr < NR; ++pr) sm[SM::RQ + pr * NR + t] = rr[pr];
@@ -1724,7 +1735,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
       DetAcc D_d, C_d;
       int DC_sg;
       lr_gj_pair<NR>(colD, &D_d, &C_d, &DC_sg);
-      if (DC_sg > 0) {
+      if (DC_sg > 0 && !(p.lr_force & 6)) {
         theta += det_log_ratio(C_d, D_d);
       } else {  // the reference's +1e-12 I retry (ledh.py:174-179), as flow_logdet
         double colC[NR];
@@ -1738,7 +1749,7 @@ __global__ void __launch_bounds__(64) k_flow_wave_lr(FlowParams p) {
           for (int r = 0; r < NR; ++r) colE[r] = ((t < NR && r == t) ? 1.0 : 0.0) + lam * m2[r];
           lr_logdet<NR>(colE, &D_d, &D_sg);
         }
-        if (C_sg * D_sg > 0) {
+        if (C_sg * D_sg > 0 && !(p.lr_force & 4)) {
           theta += det_log_ratio(C_d, D_d);
         } else {
           const double eps = 1e-12;

@@ -290,6 +290,46 @@ def test_fused_run_failure_poisons_handle(monkeypatch):
     assert np.all(np.isfinite(res.means))
 
 
+def _mat_joint_steps(monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pf, cfg, om, g = make_filter("mat_joint")
+    st = pf.init_from_gaussian(g["mean0"], g["cov0"])
+    sampler = lambda n, nx: cfg.rng.multivariate_normal(np.zeros(nx), om.Q, size=n)  # noqa: E731
+    steps = []
+    for t in range(len(g["Z"])):
+        st = pf.step(st, g["Z"][t], process_noise_sampler=sampler)
+        steps.append((st.particles.copy(), st.weights.copy(), st.mean.copy(), pf.last_resampled))
+    for k in env:
+        monkeypatch.delenv(k, raising=False)
+    return steps, max(1.0, float(np.abs(g["means"]).max()))
+
+
+@pytest.mark.parametrize("force", [1, 2, 4, 7])
+def test_flow_lr_fallbacks_equal_primary(monkeypatch, force):
+    """Advisor (round 5): k_flow_wave_lr's fallback branches, forced by a test hook
+    (PF_TEST_FLOW_LR_FORCE, FlowParams::lr_force) on the MAT joint case with the reference's recorded
+    noise - bit 0 the Householder QR instead of the Gram's Cholesky factor, bit 1 the separate pivoted
+    determinants (lr_logdet) instead of the Gauss-Jordan pair, bit 2 the reference's +1e-12 I retry
+    (ledh.py:174-179) - against the primary path: the same flow to rounding (particles 1e-9 scale,
+    weights rtol 1e-7, decisions equal); with the QR the particles are not bitwise the primary
+    path's (the forced branch did run).  The separate eliminations (bit 1) repeat the Gauss-Jordan
+    pair's pivoted arithmetic per matrix and give its determinants bit for bit, and the retry (bit 2)
+    moves every particle's log-weight by the same ~1e-9 (NX log(1 + 1e-12) per pseudo-time step),
+    which the normalised weights do not see (measured: the outputs stay bitwise equal)."""
+    ref, scale = _mat_joint_steps(monkeypatch, {})
+    got, _ = _mat_joint_steps(monkeypatch, {"PF_TEST_HOOKS": "1", "PF_TEST_FLOW_LR_FORCE": str(force)})
+    differs = False
+    for t, (a, b) in enumerate(zip(ref, got)):
+        assert a[3] == b[3], f"resample decision differs at step {t}"
+        np.testing.assert_allclose(b[0], a[0], rtol=0, atol=1e-9 * scale, err_msg=f"x t={t}")
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-13, err_msg=f"w t={t}")
+        np.testing.assert_allclose(b[2], a[2], rtol=0, atol=1e-9 * scale, err_msg=f"mean t={t}")
+        differs |= not (np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]))
+    if force & 1:
+        assert differs, "the forced QR left every output bitwise unchanged (hook not taken?)"
+
+
 def test_flow_lr_equals_dense_flow(monkeypatch):
     """Advisor (round 5): the position-space acoustic flow k_flow_wave_lr against the dense
     observation-space k_flow_wave (PF_FLOW_LR=0, read per launch) on the same inputs - the MAT
