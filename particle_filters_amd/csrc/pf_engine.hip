@@ -212,6 +212,7 @@ struct pf_handle {
   // plain-launch co-residency check (ResParams::arrive): workgroups counted so far, launch
   // sequence; after an abort the handle launches cooperatively from then on
   unsigned long long res_arrive = 0, res_seq = 0;
+  unsigned long long res_shard[RSHARDS] = {};  // k_resident's arrival shards: counts before the next launch
   bool res_force_coop = false;
   // entry header (ResParams::hdr): id of the last resident run whose exit header still
   // describes the state (0: none; any other write of the state clears it), run counter
@@ -694,9 +695,13 @@ pf_status launch_cov(pf_handle* h, const void* xs, const void* lw, int64_t s, co
 // the resident entry headers.  Allocated on first use; tags and flag values grow from launch to
 // launch (ResParams::tag0 / flag0), so the words are zeroed only when allocated or when the 32-bit
 // tag space would wrap (rsync_fits false -> rsync_reset).
-size_t rsync_bytes_needed(const pf_handle* h) {
+// k_resident's arrival shards: after the entry headers, 4 KiB aligned, RSHARD_WORDS apart
+size_t rsync_shard_offset(const pf_handle* h) {
   const size_t gran_n = RCOPIES * gran_copy_stride(h->R), flag_n = (size_t)h->R * RMAXG;
-  return (gran_n + 2 * flag_n + 4 + 4 * (size_t)h->R) * sizeof(unsigned long long);
+  return (gran_n + 2 * flag_n + 4 + 4 * (size_t)h->R + RSHARD_WORDS - 1) / RSHARD_WORDS * RSHARD_WORDS;
+}
+size_t rsync_bytes_needed(const pf_handle* h) {
+  return (rsync_shard_offset(h) + (size_t)RSHARDS * RSHARD_WORDS) * sizeof(unsigned long long);
 }
 bool rsync_fits(const pf_handle* h, int64_t T) {
   const uint64_t tag_span = 4 * (uint64_t)T + 16;
@@ -718,6 +723,7 @@ pf_status rsync_reset(pf_handle* h) {
   h->res_tag = 0;
   h->res_flag = 0;
   h->res_arrive = 0;
+  for (unsigned long long& c : h->res_shard) c = 0;
   h->res_seq = 0;
   h->res_hdr = 0;
   return PF_OK;
@@ -838,10 +844,17 @@ pf_status run_resident(pf_handle* h, const void* dZ, const void* dU, int64_t T, 
     q.arrive = h->rsync + arr_off;
     q.arrive0 = h->res_arrive;
     q.seq = ++h->res_seq;
+    const unsigned nwg = (unsigned)G * (unsigned)std::min(Rg, h->R - r0);
+    q.nshard = (int)std::min<unsigned>(RSHARDS, nwg);
+    q.arrive_sh = h->rsync + rsync_shard_offset(h);
+    for (int k = 0; k < RSHARDS; ++k) q.shard_base[k] = h->res_shard[k];
     const hipError_t e = h->ops->resident(q, G, std::min(Rg, h->R - r0), h->stream, coop,
                                           (ext0 && r0 == 0) ? h->tev[0] : nullptr,
                                           (ext1 && r0 + Rg >= h->R) ? h->tev[1] : nullptr);
-    if (e == hipSuccess) h->res_arrive += (unsigned long long)G * std::min(Rg, h->R - r0);
+    if (e == hipSuccess) {  // the shards count every workgroup, arrive[0] every shard (an aborted launch too)
+      h->res_arrive += (unsigned long long)q.nshard;
+      for (int k = 0; k < q.nshard; ++k) h->res_shard[k] += (nwg - (unsigned)k + (unsigned)q.nshard - 1) / (unsigned)q.nshard;
+    }
     if (e == hipErrorCooperativeLaunchTooLarge && r0 == 0) {
       (void)hipGetLastError();
       return PF_OK;  // not co-resident here: launch-per-step path

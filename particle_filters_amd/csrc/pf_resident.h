@@ -53,6 +53,11 @@ constexpr int RMAXG = 256;         // workgroups per replicate (<= CUs: all co-r
 constexpr int RCW = RMAXG / 64;    // waves that hold one record each per lane when verifying
 constexpr int RRING = 8;           // record ring slots (>= 2*LAG + 2)
 constexpr int RF = 8;              // record granules: M, S0 (high word), S00, S1, S2, A1, A2, S0 (low word)
+#ifndef PF_RSHARDS
+#define PF_RSHARDS 8
+#endif
+constexpr int RSHARDS = PF_RSHARDS;  // arrival count shards (res_arrive_sharded)
+constexpr int RSHARD_WORDS = 512;  // 4 KiB between shards (different lines and channels)
 #ifndef PF_RLAG
 #define PF_RLAG 2
 #endif
@@ -182,6 +187,12 @@ struct ResParams {
   // the first aborted launch's sequence number (atomicMin; all-ones when none).
   unsigned long long* arrive;
   unsigned long long arrive0, seq;
+  // Arrival shards (res_arrive_sharded): workgroup w counts itself into shard w % nshard (RSHARD_WORDS
+  // apart, values grow by the shard's workgroup count per launch from shard_base); the shard's last
+  // arrival counts the shard into arrive[0], which therefore grows by nshard per launch.
+  unsigned long long* arrive_sh;
+  unsigned long long shard_base[RSHARDS];
+  int nshard;
   int test_abort;  // test hook: the last workgroup arrives only after the others gave up
   // Entry header [R][4] {run id, lse of the exit log-weights (double bits), uniform, -}: written
   // at exit by workgroup 0 of each replicate (id hdr_out); a launch whose hdr_in matches the
@@ -261,6 +272,29 @@ __device__ __forceinline__ bool res_try_abort(unsigned long long* arrive, unsign
       return true;
     }
   }
+}
+
+// The arrival count sharded (rounds 1-5: one counter, res_arrive).  The single counter serialised the
+// launch's entry: ~245 device-scope adds on one word, ~12 ns each, the last workgroup's return ~3 us
+// after the first - on the critical path of every launch (84.0-84.5 vs 87.1-87.8 us per 20-step window
+// without it, profiles/r06/arrive).  Now workgroup w adds to shard w % nshard; the shard's LAST arrival
+// (its add returned the shard's count - 1) adds the shard to arrive[0] and leaves if that add finds an
+// abort - the linearisation point of the old protocol, now per shard.  Exclusion holds as before: a
+// workgroup passes the first verification only when every workgroup has published, so every shard's
+// last arrival has added to arrive[0] (and seen no abort) before that; res_try_abort's CAS succeeds
+// only while arrive[0] - arrive0 < nshard, i.e. before that.  A workgroup that is not its shard's last
+// proceeds without looking at arrive[0]: after an abort its shard's last arrival leaves unpublished, so
+// it never passes the first verification and leaves through res_try_abort 1 ms later (state untouched).
+// Returns 1: go on, 0: leave.  Thread 0.
+// (p: the kernel arguments in the kernarg segment - read where used, not carried in registers)
+template <class CResP>
+__device__ __forceinline__ int res_arrive_sharded(CResP p, unsigned long long sh_old) {
+  const unsigned wid = blockIdx.y * gridDim.x + blockIdx.x, nwg = gridDim.x * gridDim.y;
+  const unsigned nsh = (unsigned)p->nshard;
+  const unsigned k = wid % nsh;
+  const unsigned ck = (nwg - k + nsh - 1) / nsh;  // shard k's workgroups
+  if (sh_old - p->shard_base[k] + 1 != ck) return 1;
+  return res_arrive(p->arrive) - p->arrive0 < RABORT ? 1 : 0;
 }
 
 // A value every lane of the workgroup holds identically: move it to scalar registers.
@@ -598,8 +632,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         __builtin_amdgcn_s_sleep(8);
     __syncthreads();
   }
-  unsigned long long arr_old = 0;
-  if (t == 0) arr_old = res_arrive(p.arrive);  // its return is checked after the entry loads
+  unsigned long long arr_old = 0;  // this workgroup's shard count before its arrival
+  if (t == 0)  // its return is checked after the entry loads
+    arr_old = atomicAdd(p.arrive_sh + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % (unsigned)p.nshard) * RSHARD_WORDS, 1ull);
 #ifdef PF_STAMPS
 #ifndef PF_STAMP_T
 #define PF_STAMP_T 0
@@ -682,7 +717,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       l[e] = (i0 + e >= N) ? -INFINITY : (uniform0 ? lunif : (have_hdr ? lr[e] : lr[e] - lse0));
     if (uniform0) F0 = T0 = 0.0;
   }
-  if (t == 0) arr_sh = arr_old - KA()->arrive0 < RABORT;  // arrived after an abort: leave
+  if (t == 0) arr_sh = res_arrive_sharded(KA(), arr_old);  // arrived after an abort: leave
   __syncthreads();
   if (!arr_sh) return;
 #ifdef PF_STAMPS
@@ -1004,7 +1039,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       __syncthreads();  // every wave has read cslot[cur]
       if (!verified_any && (spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS) {
         // still no step verified after 1 ms: is the grid resident at all?
-        if (t == 0) arr_sh = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)gridDim.x * gridDim.y, KA()->seq) ? 2 : 1;
+        if (t == 0) arr_sh = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)KA()->nshard, KA()->seq) ? 2 : 1;
         __syncthreads();
         if (arr_sh == 2) {
           aborted = true;
@@ -1073,9 +1108,9 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
         while (res == 0) {
           const unsigned long long rel = ld_sc1(KA()->arrive) - KA()->arrive0;
           if (rel >= RABORT) res = 2;
-          else if (rel >= (unsigned long long)gridDim.x * gridDim.y) res = 1;
+          else if (rel >= (unsigned long long)KA()->nshard) res = 1;  // every shard counted in
           else if (__builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS)
-            res = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)gridDim.x * gridDim.y, KA()->seq) ? 2 : 1;
+            res = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)KA()->nshard, KA()->seq) ? 2 : 1;
           else
             __builtin_amdgcn_s_sleep(2);
         }
