@@ -1004,6 +1004,11 @@ pf_status check_resident(pf_handle* h) {
     HIPCHK(hipMemcpy(aw, (const void*)(h->rsync + arr_off), sizeof(aw), hipMemcpyDeviceToHost));
     HIPCHK(hipMemset((void*)(h->rsync + arr_off + 1), 0xff, sizeof(unsigned long long)));
     h->res_arrive = aw[0];
+    // k_resident's arrival shards carry the abort's marks and every arrival of the aborted launches:
+    // the next launch's bases are their values now
+    for (int k = 0; k < RSHARDS; ++k)
+      HIPCHK(hipMemcpy(&h->res_shard[k], (const void*)(h->rsync + rsync_shard_offset(h) + (size_t)k * RSHARD_WORDS),
+                       sizeof(unsigned long long), hipMemcpyDeviceToHost));
     const auto u = std::find_if(h->res_undo.begin(), h->res_undo.end(),
                                 [&](const pf_handle::ResUndo& x) { return x.seq == aw[1]; });
     if (u == h->res_undo.end()) {

@@ -188,8 +188,9 @@ struct ResParams {
   unsigned long long* arrive;
   unsigned long long arrive0, seq;
   // Arrival shards (res_arrive_sharded): workgroup w counts itself into shard w % nshard (RSHARD_WORDS
-  // apart, values grow by the shard's workgroup count per launch from shard_base); the shard's last
-  // arrival counts the shard into arrive[0], which therefore grows by nshard per launch.
+  // apart, values grow by the shard's workgroup count per launch from shard_base, +RABORT per abort
+  // mark); arrive[0] is the launch's abort decision word (res_try_abort_sharded), arrive[1] the first
+  // aborted launch's sequence number.
   unsigned long long* arrive_sh;
   unsigned long long shard_base[RSHARDS];
   int nshard;
@@ -274,27 +275,67 @@ __device__ __forceinline__ bool res_try_abort(unsigned long long* arrive, unsign
   }
 }
 
-// The arrival count sharded (rounds 1-5: one counter, res_arrive).  The single counter serialised the
-// launch's entry: ~245 device-scope adds on one word, ~12 ns each, the last workgroup's return ~3 us
-// after the first - on the critical path of every launch (84.0-84.5 vs 87.1-87.8 us per 20-step window
-// without it, profiles/r06/arrive).  Now workgroup w adds to shard w % nshard; the shard's LAST arrival
-// (its add returned the shard's count - 1) adds the shard to arrive[0] and leaves if that add finds an
-// abort - the linearisation point of the old protocol, now per shard.  Exclusion holds as before: a
-// workgroup passes the first verification only when every workgroup has published, so every shard's
-// last arrival has added to arrive[0] (and seen no abort) before that; res_try_abort's CAS succeeds
-// only while arrive[0] - arrive0 < nshard, i.e. before that.  A workgroup that is not its shard's last
-// proceeds without looking at arrive[0]: after an abort its shard's last arrival leaves unpublished, so
-// it never passes the first verification and leaves through res_try_abort 1 ms later (state untouched).
-// Returns 1: go on, 0: leave.  Thread 0.
+// Arrival (co-residency) in one uncontended round trip (rounds 1-5: one counter, res_arrive).  The
+// single counter serialised the launch's entry: ~245 device-scope adds on one word, the last workgroup's
+// return ~3 us after the first - on the critical path of every launch (84.0-84.5 vs 87.1-87.8 us per
+// 20-step window without it, profiles/r06/arrive).  Now workgroup w adds 1 to shard w % nshard
+// (RSHARD_WORDS apart; the host advances shard k's base by its workgroup count ck per launch) and
+// goes on unless that add finds an abort mark (+RABORT) on its shard.  An abort is decided once per
+// launch by the first workgroup that waits 1 ms for the first verification (res_try_abort_sharded):
+// it takes the decision word arrive[0] for this launch (CAS to seq << 2 | LOCK), adds RABORT to every
+// shard, and the abort stands iff some shard had not all its ck arrivals when marked; it stores the
+// decision (ABORT, or COMPLETE after taking its marks back).  Exclusion: a workgroup passes the first
+// verification only when every workgroup has published, i.e. every add returned no mark - all before
+// the marks, so the decision was COMPLETE; after ABORT the missing workgroup's add finds the mark and it
+// leaves unpublished, so nobody passes, and the waiting ones leave on reading ABORT (state untouched).
+// The host re-reads the shards after an abort (check_resident).  Returns 1: go on, 0: leave.  Thread 0.
 // (p: the kernel arguments in the kernarg segment - read where used, not carried in registers)
+constexpr unsigned long long RDEC_LOCK = 1, RDEC_ABORT = 2, RDEC_COMPLETE = 3;
 template <class CResP>
 __device__ __forceinline__ int res_arrive_sharded(CResP p, unsigned long long sh_old) {
-  const unsigned wid = blockIdx.y * gridDim.x + blockIdx.x, nwg = gridDim.x * gridDim.y;
   const unsigned nsh = (unsigned)p->nshard;
-  const unsigned k = wid % nsh;
-  const unsigned ck = (nwg - k + nsh - 1) / nsh;  // shard k's workgroups
-  if (sh_old - p->shard_base[k] + 1 != ck) return 1;
-  return res_arrive(p->arrive) - p->arrive0 < RABORT ? 1 : 0;
+  const unsigned k = (blockIdx.y * gridDim.x + blockIdx.x) % nsh;
+  return sh_old - p->shard_base[k] < RABORT ? 1 : 0;
+}
+template <class CResP>
+__device__ __forceinline__ bool res_try_abort_sharded(CResP p) {
+  unsigned long long* dec = p->arrive;
+  const unsigned long long mine = (unsigned long long)p->seq << 2;
+  for (;;) {
+    const unsigned long long d = ld_sc1(dec);
+    if ((d >> 2) == p->seq) {  // decided or being decided for this launch
+      if ((d & 3) == RDEC_ABORT) return true;
+      if ((d & 3) == RDEC_COMPLETE) return false;
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
+    if (atomicCAS(dec, d, mine | RDEC_LOCK) != d) continue;
+    const unsigned nsh = (unsigned)p->nshard, nwg = gridDim.x * gridDim.y;
+    bool open = false;
+    for (unsigned k = 0; k < nsh; ++k) {
+      const unsigned long long ck = (nwg - k + nsh - 1) / nsh;
+      const unsigned long long old = atomicAdd(p->arrive_sh + (size_t)k * RSHARD_WORDS, RABORT) - p->shard_base[k];
+      open |= old < ck;  // (no earlier mark in this launch: only the lock holder marks)
+    }
+    if (!open) {  // every workgroup had arrived: take the marks back, nobody arrives any more
+      for (unsigned k = 0; k < nsh; ++k) atomicAdd(p->arrive_sh + (size_t)k * RSHARD_WORDS, 0ull - RABORT);
+      __hip_atomic_exchange((gu64*)dec, mine | RDEC_COMPLETE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    atomicOr(p->err, 16u);
+    atomicMin(p->arrive + 1, p->seq);
+    __hip_atomic_exchange((gu64*)dec, mine | RDEC_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+}
+// every shard has all its arrivals and no mark (the whole grid is in); thread 0
+template <class CResP>
+__device__ __forceinline__ bool res_all_arrived(CResP p) {
+  const unsigned nsh = (unsigned)p->nshard, nwg = gridDim.x * gridDim.y;
+  bool all = true;
+  for (unsigned k = 0; k < nsh; ++k)
+    all &= ld_sc1(p->arrive_sh + (size_t)k * RSHARD_WORDS) - p->shard_base[k] == (unsigned long long)((nwg - k + nsh - 1) / nsh);
+  return all;
 }
 
 // A value every lane of the workgroup holds identically: move it to scalar registers.
@@ -628,7 +669,8 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
   __shared__ int arr_sh;
   if (p.test_abort && b == p.G - 1 && blockIdx.y == 0) {  // test hook: arrive after the others gave up
     if (t == 0)
-      while (ld_sc1(p.arrive) - p.arrive0 < RABORT && __builtin_amdgcn_s_memrealtime() - t_start < 5 * RARRIVE_TICKS)
+      while (ld_sc1(p.arrive) != (((unsigned long long)p.seq << 2) | RDEC_ABORT) &&
+             __builtin_amdgcn_s_memrealtime() - t_start < 5 * RARRIVE_TICKS)
         __builtin_amdgcn_s_sleep(8);
     __syncthreads();
   }
@@ -1039,7 +1081,7 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       __syncthreads();  // every wave has read cslot[cur]
       if (!verified_any && (spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS) {
         // still no step verified after 1 ms: is the grid resident at all?
-        if (t == 0) arr_sh = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)KA()->nshard, KA()->seq) ? 2 : 1;
+        if (t == 0) arr_sh = res_try_abort_sharded(KA()) ? 2 : 1;
         __syncthreads();
         if (arr_sh == 2) {
           aborted = true;
@@ -1106,11 +1148,11 @@ __global__ void __launch_bounds__(RBS) k_resident(ResParams p) {
       if (t == 0) {
         int res = 0;
         while (res == 0) {
-          const unsigned long long rel = ld_sc1(KA()->arrive) - KA()->arrive0;
-          if (rel >= RABORT) res = 2;
-          else if (rel >= (unsigned long long)KA()->nshard) res = 1;  // every shard counted in
+          const unsigned long long d = ld_sc1(KA()->arrive);
+          if ((d >> 2) == KA()->seq && (d & 3) == RDEC_ABORT) res = 2;
+          else if (res_all_arrived(KA())) res = 1;  // every shard complete, unmarked
           else if (__builtin_amdgcn_s_memrealtime() - t_start_sh > RARRIVE_TICKS)
-            res = res_try_abort(KA()->arrive, KA()->err, KA()->arrive0, (unsigned long long)KA()->nshard, KA()->seq) ? 2 : 1;
+            res = res_try_abort_sharded(KA()) ? 2 : 1;
           else
             __builtin_amdgcn_s_sleep(2);
         }
